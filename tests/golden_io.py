@@ -1,0 +1,62 @@
+"""Loading helpers for the committed golden fixtures (tests/golden/, made by tools/gen_golden.py)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+
+from wavelettransforms_amd import workloads as W
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+_manifest = None
+_cases = None
+
+
+def manifest():
+    global _manifest
+    if _manifest is None:
+        with open(os.path.join(GOLDEN, "manifest.json")) as fh:
+            _manifest = json.load(fh)
+    return _manifest
+
+
+def arrays():
+    global _cases
+    if _cases is None:
+        _cases = dict(np.load(os.path.join(GOLDEN, "cases.npz")))
+    return _cases
+
+
+def case_input(name):
+    rec = manifest()["cases"][name]
+    a = arrays()
+    if name + "/in" in a:
+        return a[name + "/in"]
+    seed, tid, e = rec["synth"]
+    return W.synth_numpy(tuple(rec["shape"]), seed, tid, e)
+
+
+def large_input(rec):
+    seed, tid, e = rec["synth"]
+    return W.synth_numpy(tuple(rec["shape"]), seed, tid, e)
+
+
+def canon_hash(a):
+    a = np.array(a, dtype=np.float32, copy=True).reshape(-1)
+    a[a == 0] = 0
+    return hashlib.sha256(a.tobytes()).hexdigest()
+
+
+def mask_hash(mask):
+    return hashlib.sha256(np.packbits(np.asarray(mask, bool).reshape(-1)).tobytes()).hexdigest()
+
+
+def f64_bits_equal(a, b):
+    a, b = float(a), float(b)
+    if np.isnan(a) or np.isnan(b):
+        return np.isnan(a) and np.isnan(b)
+    return np.float64(a).view(np.uint64) == np.float64(b).view(np.uint64)
+
+
+def f32_bits(x):
+    return int(np.array(x, dtype=np.float32).view(np.uint32))
