@@ -1,0 +1,130 @@
+/*
+ * wtprune.h -- C ABI of libwtprune.so, the MI355X (gfx950) implementation of the
+ * DWT -> percentile-threshold -> IDWT weight-pruning path of iAmGiG/WaveletTransforms
+ * (ResNet/dwt_pruning.py).  Plain pointers and sizes only; every device pointer is a HIP
+ * device allocation owned by the caller; every entry point is stream-ordered on the given
+ * hipStream_t (pass 0 for the null stream), never allocates, never synchronises, and is
+ * safe to capture into a hipGraph.  Status: 0 = ok, < 0 = error (wtp_last_error() has the
+ * message, phrased like the Python exception the reference would raise).
+ *
+ * Which reference interface each entry point replaces (file:line in /root/reference):
+ *   wtp_wavelet_id / wtp_dec_len    pywt.Wavelet(name).dec_len        dwt_pruning.py:13
+ *   wtp_max_level                   calculate_max_level               dwt_pruning.py:12-13
+ *   wtp_prune_f32                   multi_resolution_analysis         dwt_pruning.py:35-95
+ *                                   (per tensor of prune_layer_weights :98-127, which
+ *                                    wavelet_pruning :130-174 calls per Conv2d)
+ *   wtp_threshold_f32               percentile_based_thresholding     dwt_pruning.py:25-32
+ *   wtp_wavedec2_f32                pywt.wavedec2 + coeffs_to_array   dwt_pruning.py:67-70
+ *   wtp_waverec2_f32                array_to_coeffs + waverec2 + crop dwt_pruning.py:75-82
+ *   wtp_synth_f32                   (test/bench input generator, no reference counterpart)
+ */
+#ifndef WTPRUNE_H
+#define WTPRUNE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* wtp_stream_t; /* == hipStream_t */
+
+#define WTP_MAX_DIMS 8
+#define WTP_ABI_VERSION 1
+
+/* error codes (mirroring the exception the reference path raises) */
+#define WTP_OK 0
+#define WTP_EBADWAVELET (-1) /* ValueError: Unknown wavelet name '...'                        */
+#define WTP_EBADLEVEL (-2)   /* ValueError: Level value of L is too low . Minimum level is 0.  */
+#define WTP_EBADPCT (-3)     /* ValueError: Percentiles must be in the range [0, 100]          */
+#define WTP_EEMPTY (-4)      /* IndexError: percentile of an empty array                       */
+#define WTP_ECROP (-5)       /* IndexError/RuntimeError: the 4-index crop at :79-82 fails      */
+#define WTP_EARG (-6)        /* invalid argument (null pointer, too many dims, ...)           */
+#define WTP_EWORKSPACE (-7)  /* workspace too small                                            */
+#define WTP_EHIP (-8)        /* a HIP runtime call failed                                      */
+
+typedef struct wtp_tensor {
+    const float* in;                 /* device, contiguous C order                      */
+    float* out;                      /* device, same shape; may alias `in` (in place)   */
+    int32_t ndim;                    /* 0..8; >= 2 takes the wavelet path (:63-85)      */
+    int32_t reserved;
+    int64_t shape[WTP_MAX_DIMS];
+} wtp_tensor;
+
+/* Written by the device, one per tensor (copy back after the stream completes). */
+typedef struct wtp_result {
+    int64_t numel;          /* weights in the tensor                                 */
+    int64_t zero_count;     /* (pruned == 0).sum()        dwt_pruning.py:88-89        */
+    int64_t coeff_numel;    /* size of the packed coefficient array (percentile pop.)*/
+    double thr64;           /* np.percentile(np.abs(coeff_arr), pct)      :27        */
+    uint32_t thr32_bits;    /* float32(thr64): the compare of :31 runs in float32    */
+    uint32_t max_abs_bits;  /* np.max(np.abs(coeff_arr)) as float32 bits  :29-30     */
+    int32_t eff_level;      /* min(level, calculate_max_level(shape))     :64-65     */
+    int32_t path;           /* selection path used: 1 candidates, 2 zero-bin, 3 full scan */
+} wtp_result;
+
+/* ---- wavelets ---- */
+int wtp_abi_version(void);
+int wtp_wavelet_count(void);
+const char* wtp_wavelet_name(int wavelet_id);
+int wtp_wavelet_id(const char* name);           /* -1 if pywt would reject the name */
+int wtp_dec_len(int wavelet_id);
+int wtp_max_level(int64_t data_len, int dec_len); /* pywt.dwt_max_level */
+int wtp_packed_shape(int64_t H, int64_t W, int level, int64_t* rows, int64_t* cols);
+
+/* ---- the path: multi_resolution_analysis over a list of tensors ----
+ * Semantics per tensor t, in order (exactly dwt_pruning.py:53-89):
+ *   ndim < 2 : percentile_based_thresholding on the raw values (no wavelet check)
+ *   ndim >= 2: level = min(level, max_level(min(H, W), dec_len)) -- the clamped level
+ *              carries over to later tensors; wavedec2(periodization, axes (-2,-1));
+ *              coeffs_to_array; threshold at the pct-th percentile of |coeffs| (NumPy 1.x
+ *              linear interpolation, float32 compare); waverec2; crop; zero count.
+ * Validation happens for all tensors before any device work; on error nothing is written.
+ * Results: results_dev[t] (device memory).  Workspace: wtp_workspace_size bytes of device
+ * memory (enough for wtp_prune_f32 and wtp_prune_layers_f32 of the same tensors; 0 if the
+ * request itself is invalid), zeroed ONCE with wtp_workspace_init before first use; the library leaves it in
+ * that state after every call (it is reusable by any later call with a workspace-size
+ * request no larger than it). */
+size_t wtp_workspace_size(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level);
+int wtp_workspace_init(void* workspace, size_t bytes, wtp_stream_t stream);
+int wtp_prune_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct,
+                  void* workspace, size_t workspace_bytes, wtp_result* results_dev, wtp_stream_t stream);
+
+/* wavelet_pruning / prune_layer_weights semantics (dwt_pruning.py:98-174): every tensor is an
+ * independent call of multi_resolution_analysis([weight], ...), so the requested level is NOT
+ * carried from one tensor to the next; otherwise identical to wtp_prune_f32 (one batched
+ * launch sequence for all layers). */
+int wtp_prune_layers_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct,
+                         void* workspace, size_t workspace_bytes, wtp_result* results_dev, wtp_stream_t stream);
+
+/* percentile_based_thresholding(arr, pct) on n device floats: out = where(|in| < thr, 0, in) */
+int wtp_threshold_f32(const float* in, float* out, int64_t n, double pct, void* workspace,
+                      size_t workspace_bytes, wtp_result* result_dev, wtp_stream_t stream);
+
+/* components: batch of B images of H x W (row-major), packed coefficient array (B, rows, cols)
+ * as wtp_packed_shape; waverec2 optionally thresholds every coefficient on load with the
+ * float32 threshold read from thr32_dev (device pointer; NULL = no threshold) and crops to H x W. */
+size_t wtp_dwt_workspace_size(int64_t B, int64_t H, int64_t W, int level);
+int wtp_wavedec2_f32(const float* in, float* packed, int64_t B, int64_t H, int64_t W, int wavelet_id,
+                     int level, void* workspace, size_t workspace_bytes, wtp_stream_t stream);
+int wtp_waverec2_f32(const float* packed, float* out, int64_t B, int64_t H, int64_t W, int wavelet_id,
+                     int level, const float* thr32_dev, void* workspace, size_t workspace_bytes,
+                     wtp_stream_t stream);
+
+/* synthetic inputs (csrc/wt_synth.h): out[k] = wt_synth_value(seed, tensor_id, k, e) */
+int wtp_synth_f32(float* out, int64_t n, uint64_t seed, uint32_t tensor_id, int e, wtp_stream_t stream);
+
+/* measurement hook (bench.py): hipEvent_t handles recorded on the call's stream at the stage
+ * boundaries of later wtp_prune*_f32 calls on this thread -- [0] start, [1] forward DWT done,
+ * [2] k_hist, [3] k_findbin, [4] k_compact, [5] k_select, [6] k_mask, [7] inverse DWT done
+ * (first segment group).  n = 0 disables. */
+int wtp_set_stage_events(void* const* events, int n);
+
+const char* wtp_last_error(void);
+int wtp_last_error_tensor(void); /* index of the tensor that failed validation, or -1 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

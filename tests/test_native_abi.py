@@ -1,0 +1,91 @@
+"""CPU checks of the C-ABI library: it loads without a GPU, exports every symbol that
+include/wtprune.h declares, and its host-side logic (wavelet table, max level, packed shape,
+validation in the reference's order) matches the oracle / golden fixtures.  No kernel runs."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests import golden_io as G
+from wavelettransforms_amd import _native as N
+
+
+def test_library_exports_every_declared_symbol():
+    L = N.lib()
+    declared = N.exported_symbols()
+    assert len(declared) >= 18
+    for name in declared:
+        assert hasattr(L, name), name
+
+
+def test_wavelet_table_matches_oracle():
+    L = N.lib()
+    assert L.wtp_wavelet_count() == 106
+    for wid in range(106):
+        name = L.wtp_wavelet_name(wid).decode()
+        assert O.wavelet_id(name) == wid
+        assert L.wtp_dec_len(wid) == O.dec_len(name)
+    assert L.wtp_wavelet_id(b"nosuchwavelet") == -1
+
+
+def test_max_level_matches_pywt_table():
+    z = np.load(G.GOLDEN + "/max_level.npz")
+    L = N.lib()
+    for i, F in enumerate(z["F"]):
+        got = [L.wtp_max_level(n, int(F)) for n in range(z["table"].shape[0])]
+        assert got == list(z["table"][:, i])
+
+
+def test_packed_shape_matches_golden():
+    L = N.lib()
+    m = G.manifest()["cases"]
+    for name, rec in m.items():
+        if "error" in rec or len(rec["shape"]) < 2:
+            continue
+        pr, pc = ctypes.c_int64(), ctypes.c_int64()
+        H, W = rec["shape"][-2:]
+        assert L.wtp_packed_shape(H, W, rec["eff_level"], ctypes.byref(pr), ctypes.byref(pc)) == 0
+        assert [pr.value, pc.value] == rec["coeff_shape"][-2:], name
+
+
+def _desc(shapes):
+    arr = (N.WtpTensor * len(shapes))()
+    for i, s in enumerate(shapes):
+        arr[i].in_ = 0x1000
+        arr[i].out = 0x1000
+        arr[i].ndim = len(s)
+        for j, v in enumerate(s):
+            arr[i].shape[j] = v
+    return arr
+
+
+@pytest.mark.parametrize("shapes,wavelet,level,pct,code", [
+    ([(4, 4, 3, 3)], "nosuch", 1, 50.0, N.WTP_EBADWAVELET),
+    ([(16,)], "nosuch", 1, 50.0, None),                     # 1-D path never looks the wavelet up
+    ([(4, 4, 3, 3)], "haar", -1, 50.0, N.WTP_EBADLEVEL),
+    ([(4, 4, 3, 3)], "haar", 1, 100.5, N.WTP_EBADPCT),
+    ([(4, 4, 3, 3)], "haar", 1, float("nan"), N.WTP_EBADPCT),
+    ([(0,)], "haar", 1, 50.0, N.WTP_EEMPTY),
+    ([(33, 17)], "db4", 2, 50.0, N.WTP_ECROP),
+    ([(2, 2, 2, 18, 33)], "db2", 1, 50.0, N.WTP_ECROP),
+    ([(16,), (33, 17)], "db4", 2, 50.0, N.WTP_ECROP),        # second tensor fails, index reported
+])
+def test_validation_errors_before_any_device_work(shapes, wavelet, level, pct, code):
+    L = N.lib()
+    wid = L.wtp_wavelet_id(wavelet.encode())
+    d = _desc(shapes)
+    if code is None:
+        assert L.wtp_workspace_size(d, len(shapes), wid, level) > 0
+        return
+    rc = L.wtp_prune_f32(d, len(shapes), wid, level, pct, None, 0, 0x1000, None)
+    assert rc == code
+    assert L.wtp_last_error_tensor() == len(shapes) - 1
+    assert N.last_error()
+
+
+def test_workspace_size_covers_both_level_modes():
+    L = N.lib()
+    d = _desc([(4, 4, 3, 3), (2, 64, 64)])
+    wid = L.wtp_wavelet_id(b"haar")
+    assert L.wtp_workspace_size(d, 2, wid, 5) >= L.wtp_workspace_size(_desc([(2, 64, 64)]), 1, wid, 5)

@@ -1,0 +1,466 @@
+/*
+ * api.hip -- host side of libwtprune.so: validation in the reference's order, workspace
+ * layout, segment tables and the launch sequence of one multi_resolution_analysis call
+ * (ResNet/dwt_pruning.py:35-95).  No allocation, no synchronisation: everything is
+ * stream-ordered and graph-capturable.
+ */
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "wtp_internal.h"
+#include "wt_filters.inc"
+
+using namespace wtp;
+
+namespace {
+
+thread_local std::string g_err;
+thread_local int g_err_tensor = -1;
+thread_local hipEvent_t g_stage_ev[8];
+thread_local int g_stage_n = 0;
+
+inline void stage(int i, hipStream_t s) {
+    if (i < g_stage_n && g_stage_ev[i]) (void)hipEventRecord(g_stage_ev[i], s);
+}
+
+int fail(int code, int tensor, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+int fail(int code, int tensor, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    g_err_tensor = tensor;
+    return code;
+}
+
+constexpr size_t ALIGN = 256;
+inline size_t align_up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
+
+Taps make_taps(int wid) {
+    Taps tp;
+    memset(&tp, 0, sizeof tp);
+    const int F = wt_flen[wid];
+    tp.F = F;
+    for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < F; ++j) {
+            uint32_t b = wt_taps_bits[wt_foff[wid] + k * F + j];
+            memcpy(&tp.f[k][j], &b, 4);
+        }
+    return tp;
+}
+
+int max_level(int64_t n, int F) {
+    if (F < 2) return -1;
+    if (n < F - 1) return 0;
+    int L = 0;
+    while (((int64_t)(F - 1) << (L + 1)) <= n && L < 62) ++L;
+    return L;
+}
+
+/* One tensor of the call, as the reference would see it. */
+struct TPlan {
+    int ndim = 0;
+    int64_t numel = 0;
+    int64_t B = 1, H = 1, W = 1;
+    int L = 0;
+    bool dwt = false;     /* wavelet transform actually runs (ndim >= 2 and L >= 1)    */
+    int64_t pop = 0;      /* selection population: numel, or the packed coefficient count */
+    bool tight = true;
+    wt_level_geom g;
+    int64_t cap = 0;      /* candidate capacity                                         */
+    size_t p_off = 0;     /* workspace byte offset of the packed array (dwt only)       */
+    size_t cand_off = 0;  /* element offset into the candidate region                   */
+};
+
+struct Layout {
+    size_t hist = 0, sel = 0, cand = 0, P = 0, tmp[3] = {0, 0, 0}, total = 0;
+    size_t tmp_elems = 0;
+};
+
+bool pct_ok(double pct) { return pct >= 0.0 && pct <= 100.0; }
+
+int64_t cap_for(int64_t n) {
+    int64_t c = (n + 31) / 32;
+    if (c < 65536) c = 65536;
+    if (c > n) c = n;
+    return (c + 63) / 64 * 64;
+}
+
+/* Validate and plan every tensor in the reference's order; returns WTP_OK or the first error. */
+int plan_tensors(const wtp_tensor* ts, int n, int wid, int level, double pct, bool check_ptrs,
+                 std::vector<TPlan>& out, bool carry = true) {
+    out.assign(n, TPlan());
+    int cur_level = level;
+    for (int t = 0; t < n; ++t) {
+        if (!carry) cur_level = level;
+        const wtp_tensor& x = ts[t];
+        TPlan& p = out[t];
+        if (x.ndim < 0 || x.ndim > WTP_MAX_DIMS) return fail(WTP_EARG, t, "tensor %d: ndim %d unsupported", t, x.ndim);
+        p.ndim = x.ndim;
+        p.numel = 1;
+        for (int d = 0; d < x.ndim; ++d) {
+            if (x.shape[d] < 0) return fail(WTP_EARG, t, "tensor %d: negative dimension", t);
+            p.numel *= x.shape[d];
+        }
+        if (check_ptrs && p.numel > 0 && (!x.in || !x.out)) return fail(WTP_EARG, t, "tensor %d: null pointer", t);
+        if (x.ndim < 2) {
+            /* dwt_pruning.py:58-62 -- plain percentile, no wavelet lookup */
+            if (!pct_ok(pct)) return fail(WTP_EBADPCT, t, "Percentiles must be in the range [0, 100]");
+            if (p.numel == 0) return fail(WTP_EEMPTY, t, "index -1 is out of bounds for axis 0 with size 0");
+            p.L = cur_level;
+            p.pop = p.numel;
+        } else {
+            if (wid < 0 || wid >= WT_NUM_WAVELETS)
+                return fail(WTP_EBADWAVELET, t, "Unknown wavelet name, check wavelist() for the list of available builtin wavelets.");
+            p.H = x.shape[x.ndim - 2];
+            p.W = x.shape[x.ndim - 1];
+            p.B = 1;
+            for (int d = 0; d < x.ndim - 2; ++d) p.B *= x.shape[d];
+            const int maxL = max_level(p.H < p.W ? p.H : p.W, wt_flen[wid]);
+            if (maxL < cur_level) cur_level = maxL; /* :64-65, carried to later tensors */
+            p.L = cur_level;
+            if (p.L < 0) return fail(WTP_EBADLEVEL, t, "Level value of %d is too low . Minimum level is 0.", p.L);
+            if (p.L > 32) return fail(WTP_EARG, t, "tensor %d: level %d unsupported", t, p.L);
+            wt_geom(p.H, p.W, p.L, &p.g);
+            p.pop = p.B * p.g.PR * p.g.PC;
+            if (!pct_ok(pct)) return fail(WTP_EBADPCT, t, "Percentiles must be in the range [0, 100]");
+            if (p.pop == 0) return fail(WTP_EEMPTY, t, "index -1 is out of bounds for axis 0 with size 0");
+            p.dwt = p.L > 0;
+            if (p.dwt) {
+                int64_t nc = p.g.R[p.L] * p.g.C[p.L];
+                for (int k = 1; k <= p.L; ++k) nc += 3 * p.g.R[k] * p.g.C[k];
+                p.tight = nc == p.g.PR * p.g.PC;
+                /* waverec2 yields (2R1, 2C1); the 4-index crop of :79-82 then fails for 2-D/3-D
+                 * tensors (IndexError), cannot crop W for 5-D or anything for >= 6-D (the
+                 * later .view(original_shape) raises RuntimeError) */
+                const bool hbad = 2 * p.g.R[1] != p.H, wbad = 2 * p.g.C[1] != p.W;
+                if ((x.ndim < 4 && (hbad || wbad)) || (x.ndim == 5 && wbad) || (x.ndim >= 6 && (hbad || wbad)))
+                    return fail(WTP_ECROP, t, x.ndim < 4 ? "tuple index out of range"
+                                                         : "shape is invalid for input of this size");
+            }
+        }
+        p.cap = cap_for(p.pop);
+    }
+    return WTP_OK;
+}
+
+Layout make_layout(std::vector<TPlan>& ps) {
+    Layout L;
+    const size_t nslots = ps.size();
+    size_t off = 0;
+    L.hist = off;
+    off = align_up(off + nslots * NB_PAD * sizeof(uint32_t));
+    L.sel = off;
+    off = align_up(off + nslots * sizeof(SelState));
+    L.cand = off;
+    size_t ce = 0;
+    for (auto& p : ps) { p.cand_off = ce; ce += (size_t)p.cap; }
+    off = align_up(off + ce * sizeof(uint32_t));
+    L.P = off;
+    size_t tmp = 0;
+    for (auto& p : ps) {
+        if (!p.dwt) continue;
+        p.p_off = off;
+        off = align_up(off + (size_t)p.pop * sizeof(float));
+        const int64_t r1 = p.g.R[1], c1 = p.g.C[1];
+        const size_t a = (size_t)(p.B * r1 * (p.W > 2 * c1 ? p.W : 2 * c1));
+        const size_t b = (size_t)(p.B * 2 * r1 * 2 * c1);
+        tmp = std::max(tmp, std::max(a, b));
+    }
+    L.tmp_elems = tmp;
+    for (int i = 0; i < 3; ++i) {
+        L.tmp[i] = off;
+        off = align_up(off + tmp * sizeof(float));
+    }
+    L.total = off;
+    return L;
+}
+
+void seg_ranks(int64_t n, double pct, SegDesc& sd) {
+    /* numpy/lib/function_base.py: q = pct/100 (:4279); linear vi = (n-1)*q (:110);
+     * _get_indexes (:4730-4763): vi >= n-1 -> index -1 (the max), gamma = vi - (-1) */
+    const double q = pct / 100.0;
+    const double vi = (double)(n - 1) * q;
+    if (vi >= (double)(n - 1)) {
+        sd.above = 1;
+        sd.r0 = n - 1;
+        sd.gamma = vi - (-1.0);
+    } else {
+        const double fl = std::floor(vi);
+        sd.above = 0;
+        sd.r0 = (int64_t)fl;
+        sd.gamma = vi - fl;
+    }
+}
+
+inline char* wsb(void* ws, size_t off) { return static_cast<char*>(ws) + off; }
+
+int check_launch() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(WTP_EHIP, -1, "HIP: %s", hipGetErrorString(e));
+    return WTP_OK;
+}
+
+/* forward multi-level transform of one image batch into the packed array P */
+void forward(const float* in, const TPlan& p, const Taps& tp, float* P, float* tL, float* tH, float* tA,
+             hipStream_t s) {
+    const float* cur = in;
+    for (int k = 1; k <= p.L; ++k) {
+        launch_dwt_cols(cur, p.B, p.g.R[k - 1], p.g.C[k - 1], tp, tL, tH, s);
+        launch_dwt_rows(tL, tH, p.B, p.g.R[k], p.g.C[k - 1], tp, tA, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k],
+                        k == p.L, s);
+        cur = tA;
+    }
+}
+
+/* inverse from P (thresholded on load with *thr unless thr == nullptr), crop, zero count */
+void inverse(const float* P, const TPlan& p, const Taps& tp, const float* thr, float* out, unsigned long long* zc,
+             float* tL, float* tH, float* tA, hipStream_t s) {
+    for (int k = p.L; k >= 1; --k) {
+        const int64_t R = p.g.R[k], C = p.g.C[k];
+        const bool fromP = k == p.L;
+        const int64_t a_bs = fromP ? 0 : 4 * p.g.R[k + 1] * p.g.C[k + 1];
+        const int64_t lda = fromP ? 0 : 2 * p.g.C[k + 1];
+        launch_idwt_rows(fromP ? nullptr : tA, a_bs, lda, fromP, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k], p.B, R,
+                         C, tp, thr, tL, tH, s);
+        if (k > 1)
+            launch_idwt_cols(tL, tH, p.B, R, C, tp, tA, 2 * R, 2 * C, nullptr, s);
+        else
+            launch_idwt_cols(tL, tH, p.B, R, C, tp, out, p.H, p.W, zc, s);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int wtp_abi_version(void) { return WTP_ABI_VERSION; }
+int wtp_wavelet_count(void) { return WT_NUM_WAVELETS; }
+const char* wtp_wavelet_name(int wid) { return (wid >= 0 && wid < WT_NUM_WAVELETS) ? wt_names[wid] : nullptr; }
+int wtp_wavelet_id(const char* name) {
+    if (!name) return -1;
+    for (int i = 0; i < WT_NUM_WAVELETS; ++i)
+        if (strcmp(name, wt_names[i]) == 0) return i;
+    return -1;
+}
+int wtp_dec_len(int wid) { return (wid >= 0 && wid < WT_NUM_WAVELETS) ? wt_flen[wid] : -1; }
+int wtp_max_level(int64_t data_len, int dec_len) { return max_level(data_len, dec_len); }
+int wtp_packed_shape(int64_t H, int64_t W, int level, int64_t* rows, int64_t* cols) {
+    if (level < 0 || level > 32 || !rows || !cols) return fail(WTP_EARG, -1, "bad packed-shape request");
+    wt_level_geom g;
+    wt_geom(H, W, level, &g);
+    *rows = g.PR;
+    *cols = g.PC;
+    return WTP_OK;
+}
+const char* wtp_last_error(void) { return g_err.c_str(); }
+int wtp_set_stage_events(void* const* events, int n) {
+    if (n < 0 || n > 8 || (n > 0 && !events)) return fail(WTP_EARG, -1, "bad stage events");
+    for (int i = 0; i < 8; ++i) g_stage_ev[i] = (i < n) ? (hipEvent_t)events[i] : nullptr;
+    g_stage_n = n;
+    return WTP_OK;
+}
+int wtp_last_error_tensor(void) { return g_err_tensor; }
+
+size_t wtp_workspace_size(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level) {
+    if (ntensors < 0 || (ntensors > 0 && !tensors)) return 0;
+    /* large enough for both wtp_prune_f32 (level carried) and wtp_prune_layers_f32 */
+    std::vector<TPlan> ps, pl;
+    if (plan_tensors(tensors, ntensors, wavelet_id, level, 50.0, false, ps, true) != WTP_OK) return 0;
+    if (plan_tensors(tensors, ntensors, wavelet_id, level, 50.0, false, pl, false) != WTP_OK) return 0;
+    return std::max(make_layout(ps).total, make_layout(pl).total);
+}
+
+int wtp_workspace_init(void* ws, size_t bytes, wtp_stream_t stream) {
+    if (!ws && bytes) return fail(WTP_EARG, -1, "null workspace");
+    if (bytes && hipMemsetAsync(ws, 0, bytes, (hipStream_t)stream) != hipSuccess)
+        return fail(WTP_EHIP, -1, "hipMemsetAsync failed");
+    return WTP_OK;
+}
+
+static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, void* ws,
+                      size_t ws_bytes, wtp_result* results, wtp_stream_t stream, bool carry) {
+    g_err.clear();
+    g_err_tensor = -1;
+    if (ntensors < 0 || (ntensors > 0 && (!tensors || !results))) return fail(WTP_EARG, -1, "bad arguments");
+    if (ntensors == 0) return WTP_OK;
+    std::vector<TPlan> ps;
+    int rc = plan_tensors(tensors, ntensors, wavelet_id, level, pct, true, ps, carry);
+    if (rc != WTP_OK) return rc;
+    Layout lay = make_layout(ps);
+    if (!ws || ws_bytes < lay.total)
+        return fail(WTP_EWORKSPACE, -1, "workspace too small: need %zu bytes, got %zu", lay.total, ws_bytes);
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t* hist = reinterpret_cast<uint32_t*>(wsb(ws, lay.hist));
+    SelState* sel = reinterpret_cast<SelState*>(wsb(ws, lay.sel));
+    uint32_t* cand = reinterpret_cast<uint32_t*>(wsb(ws, lay.cand));
+    float* tL = reinterpret_cast<float*>(wsb(ws, lay.tmp[0]));
+    float* tH = reinterpret_cast<float*>(wsb(ws, lay.tmp[1]));
+    float* tA = reinterpret_cast<float*>(wsb(ws, lay.tmp[2]));
+    const Taps tp = (wavelet_id >= 0 && wavelet_id < WT_NUM_WAVELETS) ? make_taps(wavelet_id) : Taps{};
+
+    stage(0, s);
+    /* 1. forward transforms into the packed arrays (pywt.wavedec2 + coeffs_to_array) */
+    for (int t = 0; t < ntensors; ++t) {
+        const TPlan& p = ps[t];
+        if (!p.dwt) continue;
+        float* P = reinterpret_cast<float*>(wsb(ws, p.p_off));
+        if (!p.tight && hipMemsetAsync(P, 0, (size_t)p.pop * sizeof(float), s) != hipSuccess)
+            return fail(WTP_EHIP, t, "hipMemsetAsync failed");
+        forward(tensors[t].in, p, tp, P, tL, tH, tA, s);
+    }
+    /* 2. exact percentile selection + level-0 mask, SEG_PER_LAUNCH segments per launch group */
+    for (int g0 = 0; g0 < ntensors; g0 += SEG_PER_LAUNCH) {
+        SegTable tab;
+        memset(&tab, 0, sizeof tab);
+        int blk = 0;
+        for (int t = g0; t < ntensors && t < g0 + SEG_PER_LAUNCH; ++t) {
+            const TPlan& p = ps[t];
+            SegDesc& sd = tab.s[tab.nseg++];
+            sd.data = p.dwt ? reinterpret_cast<const float*>(wsb(ws, p.p_off)) : tensors[t].in;
+            sd.out = p.dwt ? nullptr : tensors[t].out;
+            sd.n = p.pop;
+            seg_ranks(p.pop, pct, sd);
+            sd.numel = p.numel;
+            sd.blk_begin = blk;
+            sd.slot = t;
+            sd.res = t;
+            sd.eff_level = p.L;
+            sd.flags = p.dwt ? 0 : SEG_MASK;
+            const uintptr_t a = reinterpret_cast<uintptr_t>(sd.data), o = reinterpret_cast<uintptr_t>(sd.out);
+            if ((a % 16) == 0 && (o % 16) == 0) sd.flags |= SEG_ALIGNED;
+            sd.cand_off = (int64_t)p.cand_off;
+            sd.cap = p.cap;
+            blk += (int)((p.pop + CHUNK - 1) / CHUNK);
+        }
+        tab.nblk = blk;
+        const bool first = g0 == 0;
+        if (first) stage(1, s);
+        launch_hist(tab, hist, sel, s);
+        if (first) stage(2, s);
+        launch_findbin(tab, hist, sel, results, s);
+        if (first) stage(3, s);
+        launch_compact(tab, sel, cand, s);
+        if (first) stage(4, s);
+        launch_select(tab, sel, cand, results, s);
+        if (first) stage(5, s);
+        launch_mask(tab, sel, results, s);
+        if (first) stage(6, s);
+    }
+    /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2) */
+    for (int t = 0; t < ntensors; ++t) {
+        const TPlan& p = ps[t];
+        if (!p.dwt) continue;
+        const float* P = reinterpret_cast<const float*>(wsb(ws, p.p_off));
+        inverse(P, p, tp, &sel[t].thr32, tensors[t].out,
+                reinterpret_cast<unsigned long long*>(&results[t].zero_count), tL, tH, tA, s);
+    }
+    stage(7, s);
+    return check_launch();
+}
+
+int wtp_prune_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, void* ws,
+                  size_t ws_bytes, wtp_result* results, wtp_stream_t stream) {
+    return prune_impl(tensors, ntensors, wavelet_id, level, pct, ws, ws_bytes, results, stream, true);
+}
+
+int wtp_prune_layers_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, void* ws,
+                         size_t ws_bytes, wtp_result* results, wtp_stream_t stream) {
+    return prune_impl(tensors, ntensors, wavelet_id, level, pct, ws, ws_bytes, results, stream, false);
+}
+
+int wtp_threshold_f32(const float* in, float* out, int64_t n, double pct, void* ws, size_t ws_bytes,
+                      wtp_result* result, wtp_stream_t stream) {
+    wtp_tensor t;
+    memset(&t, 0, sizeof t);
+    t.in = in;
+    t.out = out;
+    t.ndim = 1;
+    t.shape[0] = n;
+    return wtp_prune_f32(&t, 1, -1, 0, pct, ws, ws_bytes, result, stream);
+}
+
+size_t wtp_dwt_workspace_size(int64_t B, int64_t H, int64_t W, int level) {
+    if (level <= 0) return 0;
+    wt_level_geom g;
+    wt_geom(H, W, level, &g);
+    const size_t a = (size_t)(B * g.R[1] * (W > 2 * g.C[1] ? W : 2 * g.C[1]));
+    const size_t b = (size_t)(B * 2 * g.R[1] * 2 * g.C[1]);
+    return 3 * align_up(std::max(a, b) * sizeof(float));
+}
+
+static int component_plan(int64_t B, int64_t H, int64_t W, int wid, int level, TPlan& p) {
+    if (wid < 0 || wid >= WT_NUM_WAVELETS) return fail(WTP_EBADWAVELET, -1, "Unknown wavelet name");
+    if (level < 0) return fail(WTP_EBADLEVEL, -1, "Level value of %d is too low . Minimum level is 0.", level);
+    if (level > 32 || B < 0 || H <= 0 || W <= 0) return fail(WTP_EARG, -1, "bad component arguments");
+    p.B = B;
+    p.H = H;
+    p.W = W;
+    p.L = level;
+    p.dwt = level > 0;
+    wt_geom(H, W, level, &p.g);
+    p.pop = B * p.g.PR * p.g.PC;
+    int64_t nc = p.g.R[level] * p.g.C[level];
+    for (int k = 1; k <= level; ++k) nc += 3 * p.g.R[k] * p.g.C[k];
+    p.tight = nc == p.g.PR * p.g.PC;
+    return WTP_OK;
+}
+
+int wtp_wavedec2_f32(const float* in, float* packed, int64_t B, int64_t H, int64_t W, int wid, int level, void* ws,
+                     size_t ws_bytes, wtp_stream_t stream) {
+    TPlan p;
+    int rc = component_plan(B, H, W, wid, level, p);
+    if (rc != WTP_OK) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    if (level == 0) {
+        if (hipMemcpyAsync(packed, in, (size_t)(B * H * W) * sizeof(float), hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return fail(WTP_EHIP, -1, "hipMemcpyAsync failed");
+        return WTP_OK;
+    }
+    const size_t need = wtp_dwt_workspace_size(B, H, W, level);
+    if (!ws || ws_bytes < need) return fail(WTP_EWORKSPACE, -1, "workspace too small: need %zu", need);
+    const size_t one = need / 3;
+    float* tL = reinterpret_cast<float*>(wsb(ws, 0));
+    float* tH = reinterpret_cast<float*>(wsb(ws, one));
+    float* tA = reinterpret_cast<float*>(wsb(ws, 2 * one));
+    if (!p.tight && hipMemsetAsync(packed, 0, (size_t)p.pop * sizeof(float), s) != hipSuccess)
+        return fail(WTP_EHIP, -1, "hipMemsetAsync failed");
+    forward(in, p, make_taps(wid), packed, tL, tH, tA, s);
+    return check_launch();
+}
+
+int wtp_waverec2_f32(const float* packed, float* out, int64_t B, int64_t H, int64_t W, int wid, int level,
+                     const float* thr32, void* ws, size_t ws_bytes, wtp_stream_t stream) {
+    TPlan p;
+    int rc = component_plan(B, H, W, wid, level, p);
+    if (rc != WTP_OK) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    if (level == 0) {
+        launch_copy_threshold(packed, out, B * H * W, thr32, nullptr, s);
+        return check_launch();
+    }
+    const size_t need = wtp_dwt_workspace_size(B, H, W, level);
+    if (!ws || ws_bytes < need) return fail(WTP_EWORKSPACE, -1, "workspace too small: need %zu", need);
+    const size_t one = need / 3;
+    float* tL = reinterpret_cast<float*>(wsb(ws, 0));
+    float* tH = reinterpret_cast<float*>(wsb(ws, one));
+    float* tA = reinterpret_cast<float*>(wsb(ws, 2 * one));
+    inverse(packed, p, make_taps(wid), thr32, out, nullptr, tL, tH, tA, s);
+    return check_launch();
+}
+
+int wtp_synth_f32(float* out, int64_t n, uint64_t seed, uint32_t tensor_id, int e, wtp_stream_t stream) {
+    if (n < 0 || (n > 0 && !out)) return fail(WTP_EARG, -1, "bad synth arguments");
+    if (n == 0) return WTP_OK;
+    launch_synth(out, n, seed, tensor_id, e, (hipStream_t)stream);
+    return check_launch();
+}
+
+}  // extern "C"

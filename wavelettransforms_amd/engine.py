@@ -1,0 +1,210 @@
+"""Device-resident execution of the DWT -> percentile-threshold -> IDWT path for torch tensors.
+
+`launch()` issues one batched launch sequence (libwtprune.so) for a list of CUDA float32
+tensors on the current stream and returns the outputs plus the device-side result records;
+`prune()` additionally waits and decodes them.  Nothing here computes on the CPU: the
+numbers come from the HIP kernels, the host only packs pointers and decodes results.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+RESULT_DTYPE = np.dtype([("numel", "<i8"), ("zero_count", "<i8"), ("coeff_numel", "<i8"), ("thr64", "<f8"),
+                         ("thr32_bits", "<u4"), ("max_abs_bits", "<u4"), ("eff_level", "<i4"), ("path", "<i4")])
+assert RESULT_DTYPE.itemsize == N.RESULT_BYTES
+
+_workspaces = {}
+
+
+def wavelet_id(name):
+    return N.lib().wtp_wavelet_id(str(name).encode()) if isinstance(name, str) else -1
+
+
+def workspace(device, nbytes):
+    """Grow-only, zero-initialised workspace per device (the library keeps it clean between calls)."""
+    device = torch.device(device)
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    ws = _workspaces.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _workspaces[key] = ws
+    return ws
+
+
+def _as_desc(tensors, outs):
+    arr = (N.WtpTensor * max(1, len(tensors)))()
+    for i, (x, y) in enumerate(zip(tensors, outs)):
+        d = arr[i]
+        d.in_ = x.data_ptr() if x.numel() else None
+        d.out = y.data_ptr() if y.numel() else None
+        d.ndim = x.dim()
+        for j, s in enumerate(x.shape):
+            d.shape[j] = s
+    return arr
+
+
+def raise_for(code, tensors, wavelet):
+    """Map a library status to the exception the reference path raises at that point."""
+    L = N.lib()
+    msg = N.last_error()
+    t = L.wtp_last_error_tensor()
+    if code == N.WTP_EBADWAVELET:
+        raise ValueError("Unknown wavelet name '%s', check wavelist() for the list of available builtin "
+                         "wavelets." % wavelet)
+    if code in (N.WTP_EBADLEVEL, N.WTP_EBADPCT):
+        raise ValueError(msg)
+    if code == N.WTP_EEMPTY:
+        raise IndexError(msg)
+    if code == N.WTP_ECROP:
+        x = tensors[t] if 0 <= t < len(tensors) else None
+        if x is not None and x.dim() > 4:
+            raise RuntimeError("shape '%s' is invalid for input of size %d" % (list(x.shape), _recon_numel(x)))
+        raise IndexError(msg)
+    raise RuntimeError("libwtprune: %s (status %d)" % (msg, code))
+
+
+def _recon_numel(x):
+    # size of the waverec2 output after the reference's 4-index crop (for the error message)
+    shape = list(x.shape)
+    h, w = shape[-2], shape[-1]
+    shape[-1] = 2 * ((w + 1) // 2)
+    if x.dim() >= 6:
+        shape[-2] = 2 * ((h + 1) // 2)
+    n = 1
+    for s in shape:
+        n *= s
+    return n
+
+
+def check_tensors(tensors):
+    for x in tensors:
+        if not isinstance(x, torch.Tensor):
+            raise TypeError("expected torch.Tensor, got %r" % type(x))
+        if not x.is_cuda:
+            raise ValueError("wavelettransforms_amd runs on the GPU: tensor on %s (move it to cuda)" % x.device)
+        if x.dtype != torch.float32:
+            raise TypeError("wavelettransforms_amd: float32 weights only (got %s)" % x.dtype)
+
+
+def launch(tensors, wavelet, level, pct, outs=None, carry_level=True, stream=None):
+    """Enqueue the path for `tensors` (CUDA float32) on `stream` (default: current stream).
+    Returns (outs, results_dev) without synchronising; results_dev is a uint8 CUDA tensor of
+    len(tensors) wtp_result records.  carry_level=True is multi_resolution_analysis over a
+    list (the clamped level carries over, dwt_pruning.py:64-65); False is one call per layer
+    (prune_layer_weights / wavelet_pruning)."""
+    check_tensors(tensors)
+    tensors = [x.contiguous() for x in tensors]
+    if outs is None:
+        outs = [torch.empty_like(x) for x in tensors]
+    n = len(tensors)
+    if n == 0:
+        return outs, None
+    device = tensors[0].device
+    L = N.lib()
+    wid = wavelet_id(wavelet)
+    desc = _as_desc(tensors, outs)
+    nbytes = L.wtp_workspace_size(desc, n, wid, int(level))
+    ws = workspace(device, nbytes if nbytes else 256)
+    res = torch.empty(n * N.RESULT_BYTES, dtype=torch.uint8, device=device)
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    fn = L.wtp_prune_f32 if carry_level else L.wtp_prune_layers_f32
+    rc = fn(desc, n, wid, int(level), float(pct), ws.data_ptr(), ws.numel(), res.data_ptr(),
+            ctypes.c_void_p(stream.cuda_stream))
+    if rc != N.WTP_OK:
+        raise_for(rc, tensors, wavelet)
+    return outs, res
+
+
+def decode(results_dev, n):
+    host = results_dev.cpu().numpy().view(RESULT_DTYPE)[:n]
+    out = []
+    for r in host:
+        d = {k: r[k].item() for k in RESULT_DTYPE.names}
+        d["thr32"] = float(np.array(d["thr32_bits"], np.uint32).view(np.float32))
+        d["max_abs"] = np.array(d["max_abs_bits"], np.uint32).view(np.float32)[()]
+        d["nonzero"] = d["numel"] - d["zero_count"]
+        out.append(d)
+    return out
+
+
+def prune(tensors, wavelet, level, pct, outs=None, carry_level=True):
+    """launch() + wait + decoded per-tensor records (numel, zero_count, nonzero, thr64, ...)."""
+    outs, res = launch(tensors, wavelet, level, pct, outs=outs, carry_level=carry_level)
+    if res is None:
+        return outs, []
+    return outs, decode(res, len(tensors))
+
+
+def threshold(x, pct, out=None):
+    """percentile_based_thresholding (dwt_pruning.py:25-32) of a CUDA float32 tensor."""
+    check_tensors([x])
+    x = x.contiguous()
+    out = torch.empty_like(x) if out is None else out
+    L = N.lib()
+    desc = _as_desc([x.reshape(-1)], [out.reshape(-1)])
+    ws = workspace(x.device, L.wtp_workspace_size(desc, 1, -1, 0) or 256)
+    res = torch.empty(N.RESULT_BYTES, dtype=torch.uint8, device=x.device)
+    rc = L.wtp_threshold_f32(x.data_ptr() if x.numel() else None, out.data_ptr() if x.numel() else None,
+                             x.numel(), float(pct), ws.data_ptr(), ws.numel(), res.data_ptr(),
+                             ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+    if rc != N.WTP_OK:
+        raise_for(rc, [x], None)
+    return out, decode(res, 1)[0]
+
+
+def wavedec2_packed(x, wavelet, level):
+    """pywt.coeffs_to_array(pywt.wavedec2(x, wavelet, level, 'periodization', axes=(-2,-1)))[0] on the GPU."""
+    check_tensors([x])
+    x = x.contiguous()
+    L = N.lib()
+    H, W = x.shape[-2], x.shape[-1]
+    B = x.numel() // max(1, H * W)
+    pr, pc = ctypes.c_int64(), ctypes.c_int64()
+    if L.wtp_packed_shape(H, W, int(level), ctypes.byref(pr), ctypes.byref(pc)) != 0:
+        raise ValueError(N.last_error())
+    P = torch.empty(tuple(x.shape[:-2]) + (pr.value, pc.value), dtype=torch.float32, device=x.device)
+    nb = L.wtp_dwt_workspace_size(B, H, W, int(level))
+    ws = torch.empty(max(nb, 256), dtype=torch.uint8, device=x.device)
+    rc = L.wtp_wavedec2_f32(x.data_ptr(), P.data_ptr(), B, H, W, wavelet_id(wavelet), int(level), ws.data_ptr(),
+                            ws.numel(), ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+    if rc != 0:
+        raise_for(rc, [x], wavelet)
+    return P
+
+
+def waverec2_packed(P, shape, wavelet, level, thr32=None):
+    """array_to_coeffs + waverec2 + crop to `shape` (optionally thresholding on load)."""
+    L = N.lib()
+    H, W = shape[-2], shape[-1]
+    B = 1
+    for s in shape[:-2]:
+        B *= s
+    out = torch.empty(tuple(shape), dtype=torch.float32, device=P.device)
+    nb = L.wtp_dwt_workspace_size(B, H, W, int(level))
+    ws = torch.empty(max(nb, 256), dtype=torch.uint8, device=P.device)
+    thr = None
+    if thr32 is not None:
+        thr = torch.tensor([thr32], dtype=torch.float32, device=P.device)
+    rc = L.wtp_waverec2_f32(P.contiguous().data_ptr(), out.data_ptr(), B, H, W, wavelet_id(wavelet), int(level),
+                            thr.data_ptr() if thr is not None else None, ws.data_ptr(), ws.numel(),
+                            ctypes.c_void_p(torch.cuda.current_stream(P.device).cuda_stream))
+    if rc != 0:
+        raise_for(rc, [P], wavelet)
+    return out
+
+
+def synth(shape, seed, tensor_id, e, device="cuda"):
+    """Synthetic weights on the device (csrc/wt_synth.h), identical to workloads.synth_numpy."""
+    n = 1
+    for s in shape:
+        n *= s
+    out = torch.empty(tuple(shape), dtype=torch.float32, device=device)
+    rc = N.lib().wtp_synth_f32(out.data_ptr() if n else None, n, seed, tensor_id, int(e),
+                               ctypes.c_void_p(torch.cuda.current_stream(out.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError(N.last_error())
+    return out
