@@ -28,9 +28,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "weight-coeffs/s for L5 bior3.3 DWT+thresh+IDWT; achieved HBM GB/s vs peak"
-STAGES = ["forward_dwt", "k_hist", "k_findbin", "k_compact", "k_select", "k_mask", "inverse_dwt"]
-KERNEL_OF_STAGE = {"k_hist": "k_hist", "k_findbin": "k_findbin", "k_compact": "k_compact",
-                   "k_select": "k_select", "k_mask": "k_mask"}
+STAGES = ["forward_dwt", "k_sample", "k_collect", "k_select", "k_mask", "inverse_dwt"]
+KERNEL_OF_STAGE = {"k_sample": "k_sample", "k_collect": "k_collect", "k_select": "k_select", "k_mask": "k_mask"}
 
 
 def parse():
@@ -64,8 +63,8 @@ def stage_bytes(stage, n_w, pop, has_dwt):
     """Algorithmic bytes each stage must move (4 B read of w + 4 B write of w')."""
     if stage in ("forward_dwt", "inverse_dwt") and not has_dwt:
         return 0
-    return {"forward_dwt": 4 * n_w + 4 * pop, "k_hist": 4 * pop, "k_findbin": 0, "k_compact": 4 * pop,
-            "k_select": 0, "k_mask": 8 * n_w if pop == n_w else 0, "inverse_dwt": 4 * pop + 4 * n_w}[stage]
+    return {"forward_dwt": 4 * n_w + 4 * pop, "k_sample": 0, "k_collect": 4 * pop, "k_select": 0,
+            "k_mask": 8 * n_w if pop == n_w else 0, "inverse_dwt": 4 * pop + 4 * n_w}[stage]
 
 
 def pmc_traffic(config, kernel):
@@ -155,14 +154,14 @@ def main():
     value = world * n_w * K / T
 
     # ---- per-stage device durations (HIP events on the library's stream, queue pre-filled) ----
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(8)]
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(STAGES) + 1)]
     for e in evs:
         e.record()
     torch.cuda.synchronize()
-    handles = (ctypes.c_void_p * 8)(*[e.cuda_event for e in evs])
+    handles = (ctypes.c_void_p * len(evs))(*[e.cuda_event for e in evs])
     filler = torch.empty(128 << 20, dtype=torch.float32, device=dev)
     per = {st: [] for st in STAGES}
-    N.lib().wtp_set_stage_events(handles, 8)
+    N.lib().wtp_set_stage_events(handles, len(evs))
     try:
         for _ in range(args.stage_reps):
             filler.mul_(1.0)  # ~0.2 ms of device work so the whole call is enqueued before it runs

@@ -61,7 +61,7 @@ typedef struct wtp_result {
     uint32_t thr32_bits;    /* float32(thr64): the compare of :31 runs in float32    */
     uint32_t max_abs_bits;  /* np.max(np.abs(coeff_arr)) as float32 bits  :29-30     */
     int32_t eff_level;      /* min(level, calculate_max_level(shape))     :64-65     */
-    int32_t path;           /* selection path used: 1 candidates, 2 zero-bin, 3 full scan */
+    int32_t path;           /* selection: 1 window candidates, 2 window edges, 3 full scan */
 } wtp_result;
 
 /* ---- wavelets ---- */
@@ -117,8 +117,8 @@ int wtp_synth_f32(float* out, int64_t n, uint64_t seed, uint32_t tensor_id, int 
 
 /* measurement hook (bench.py): hipEvent_t handles recorded on the call's stream at the stage
  * boundaries of later wtp_prune*_f32 calls on this thread -- [0] start, [1] forward DWT done,
- * [2] k_hist, [3] k_findbin, [4] k_compact, [5] k_select, [6] k_mask, [7] inverse DWT done
- * (first segment group).  n = 0 disables. */
+ * [2] k_sample, [3] k_collect, [4] k_select, [5] k_mask, [6] inverse DWT done (first segment
+ * group).  n = 0 disables. */
 int wtp_set_stage_events(void* const* events, int n);
 
 const char* wtp_last_error(void);

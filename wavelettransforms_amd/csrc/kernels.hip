@@ -2,12 +2,14 @@
  * kernels.hip -- gfx950 kernels of the DWT -> percentile-threshold -> IDWT path.
  *
  * Selection (np.percentile(np.abs(coeff_arr), pct) + np.where(|c| < thr, 0, c),
- * ResNet/dwt_pruning.py:25-32) over grouped segments, one segment per tensor:
- *   k_hist     stream |x| once: 4099-bin LDS histogram of the |x| bit pattern + max key
- *   k_findbin  one block per segment: locate the bins of order statistics r0, r0+1
- *   k_compact  stream again (Infinity-Cache resident): gather the keys of those bins
- *   k_select   one block per segment: exact radix select among the candidates, NumPy 1.x
- *              linear interpolation in f64, float32 threshold
+ * ResNet/dwt_pruning.py:25-32) over grouped segments, one segment per tensor, on the float32
+ * bit pattern of |x| (a key monotone in |x|; NaN sorts last as in np.partition):
+ *   k_sample   one block per segment: 32768 sampled keys -> window [kl, kh] bracketing the
+ *              order statistics r0, r0+1 (exact keys when the segment fits in the sample)
+ *   k_collect  stream once: count keys < kl, == kl, == kh; gather keys inside (kl, kh)
+ *              with a 256-bin sub-histogram; max key
+ *   k_select   one block per segment: exact radix select of both ranks (inside candidates,
+ *              or the whole segment if the window missed), NumPy 1.x _lerp in f64
  *   k_mask     stream again: out = |x| < thr ? 0 : x, zero count        (level-0 segments)
  * Filter bank (pywt.wavedec2 / waverec2 periodization, :67-77): separable one-level passes
  * whose every output is summed in PyWavelets' exact order (csrc/wt_dwt_core.h); the
@@ -74,168 +76,7 @@ __device__ __forceinline__ void load_chunk(const float* p, float4 (&v)[16]) {
     for (int it = 0; it < 16; ++it) v[it] = p4[it * STREAM_THREADS + threadIdx.x];
 }
 
-/* ----------------------------------------------------------------- k_hist --- */
-__global__ __launch_bounds__(STREAM_THREADS) void k_hist(SegTable t, uint32_t* __restrict__ hist,
-                                                         SelState* __restrict__ sel) {
-    __shared__ uint32_t h[NB];
-    const int si = find_seg(t, blockIdx.x);
-    const SegDesc& sd = t.s[si];
-    const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * CHUNK;
-    const int64_t len = min((int64_t)CHUNK, sd.n - base);
-    for (int i = threadIdx.x; i < NB; i += STREAM_THREADS) h[i] = 0;
-    __syncthreads();
-    uint32_t mx = 0;
-    const float* p = sd.data + base;
-    auto put = [&](float x) {
-        const uint32_t k = abs_key(x);
-        mx = max(mx, k);
-        atomicAdd(&h[key_bin(k)], 1u);
-    };
-    if ((sd.flags & SEG_ALIGNED) && len == CHUNK) {
-        float4 v[16];
-        load_chunk(p, v);
-#pragma unroll
-        for (int it = 0; it < 16; ++it) { put(v[it].x); put(v[it].y); put(v[it].z); put(v[it].w); }
-    } else {
-        for (int64_t i = threadIdx.x; i < len; i += STREAM_THREADS) put(p[i]);
-    }
-    mx = wave_max_u32(mx);
-    if ((threadIdx.x & 63) == 0) atomicMax(&sel[sd.slot].maxkey, mx);
-    __syncthreads();
-    uint32_t* g = hist + (size_t)sd.slot * NB_PAD;
-    for (int i = threadIdx.x; i < NB; i += STREAM_THREADS) {
-        const uint32_t c = h[i];
-        if (c) atomicAdd(&g[i], c);
-    }
-}
-
-/* -------------------------------------------------------------- k_findbin --- */
-constexpr int FB_THREADS = 1024;
-constexpr int FB_PER = (NB + FB_THREADS - 1) / FB_THREADS; /* 5 bins per thread */
-
-__global__ __launch_bounds__(FB_THREADS) void k_findbin(SegTable t, uint32_t* __restrict__ hist,
-                                                        SelState* __restrict__ sel, wtp_result* __restrict__ res) {
-    __shared__ uint32_t h[FB_PER * FB_THREADS];
-    __shared__ int64_t wtot[FB_THREADS / 64];
-    __shared__ int64_t found[4]; /* bin0, before0, bin1, before1 */
-    const SegDesc& sd = t.s[blockIdx.x];
-    uint32_t* g = hist + (size_t)sd.slot * NB_PAD;
-    if (threadIdx.x < 4) found[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i < FB_PER * FB_THREADS; i += FB_THREADS) {
-        uint32_t c = 0;
-        if (i < NB) { c = g[i]; g[i] = 0; } /* read and leave the slot zeroed for the next call */
-        h[i] = c;
-    }
-    __syncthreads();
-    int64_t local = 0;
-#pragma unroll
-    for (int j = 0; j < FB_PER; ++j) local += h[threadIdx.x * FB_PER + j];
-    const int64_t incl = wave_incl_scan(local);
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 63) wtot[wv] = incl;
-    __syncthreads();
-    int64_t wbase = 0;
-    for (int i = 0; i < wv; ++i) wbase += wtot[i];
-    int64_t cum = wbase + incl - local;
-    const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
-#pragma unroll
-    for (int j = 0; j < FB_PER; ++j) {
-        const int b = threadIdx.x * FB_PER + j;
-        const int64_t c = h[b];
-        if (c) {
-            if (r0 >= cum && r0 < cum + c) { found[0] = b; found[1] = cum; }
-            if (r1 >= cum && r1 < cum + c) { found[2] = b; found[3] = cum; }
-        }
-        cum += c;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        SelState& st = sel[sd.slot];
-        const int bin0 = (int)found[0], bin1 = (int)found[2];
-        st.a_zero = bin0 == BIN_ZERO;
-        st.b_zero = bin1 == BIN_ZERO;
-        if (bin1 == BIN_ZERO) {
-            st.mode = MODE_ZERO;
-            st.cb_lo = 1;
-            st.cb_hi = 0;
-            st.below = 0;
-        } else {
-            /* bins strictly between two adjacent order statistics are empty, so the
-             * candidate range is [bin0, bin1] (or just bin1 when r0 is an exact zero) */
-            const int lo = (bin0 == BIN_ZERO) ? bin1 : bin0;
-            const int64_t below = (bin0 == BIN_ZERO) ? found[3] : found[1];
-            const int64_t count = found[3] + (int64_t)h[bin1] - below;
-            st.cb_lo = lo;
-            st.cb_hi = bin1;
-            st.below = below;
-            st.mode = (count <= sd.cap) ? MODE_CAND : MODE_FULL;
-        }
-        res[sd.res].zero_count = 0;
-    }
-}
-
-/* -------------------------------------------------------------- k_compact --- */
-__global__ __launch_bounds__(STREAM_THREADS) void k_compact(SegTable t, SelState* __restrict__ sel,
-                                                            uint32_t* __restrict__ cand) {
-    __shared__ int wtot[STREAM_THREADS / 64];
-    __shared__ uint32_t sbase;
-    const int si = find_seg(t, blockIdx.x);
-    const SegDesc& sd = t.s[si];
-    SelState* st = sel + sd.slot;
-    if (st->mode != MODE_CAND) return;
-    const uint32_t blo = st->cb_lo, bhi = st->cb_hi;
-    const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * CHUNK;
-    const int64_t len = min((int64_t)CHUNK, sd.n - base);
-    const float* p = sd.data + base;
-    const bool full = (sd.flags & SEG_ALIGNED) && len == CHUNK;
-    float4 v[16];
-    int cnt = 0;
-    auto hit = [&](float x) {
-        const uint32_t b = (uint32_t)key_bin(abs_key(x));
-        return b >= blo && b <= bhi;
-    };
-    if (full) {
-        load_chunk(p, v);
-#pragma unroll
-        for (int it = 0; it < 16; ++it) cnt += hit(v[it].x) + hit(v[it].y) + hit(v[it].z) + hit(v[it].w);
-    } else {
-        for (int64_t i = threadIdx.x; i < len; i += STREAM_THREADS) cnt += hit(p[i]);
-    }
-    /* block exclusive scan of per-thread counts */
-    const int incl = (int)wave_incl_scan(cnt);
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 63) wtot[wv] = incl;
-    __syncthreads();
-    int off = incl - cnt, total = 0;
-    for (int i = 0; i < STREAM_THREADS / 64; ++i) {
-        if (i < wv) off += wtot[i];
-        total += wtot[i];
-    }
-    if (threadIdx.x == 0) sbase = total ? atomicAdd(&st->cand_count, (uint32_t)total) : 0u;
-    __syncthreads();
-    if (!cnt) return;
-    const int64_t cap = sd.cap;
-    uint32_t* out = cand + sd.cand_off;
-    int64_t pos = (int64_t)sbase + off;
-    auto emit = [&](float x) {
-        const uint32_t k = abs_key(x);
-        const uint32_t b = (uint32_t)key_bin(k);
-        if (b >= blo && b <= bhi) {
-            if (pos < cap) out[pos] = k;
-            ++pos;
-        }
-    };
-    if (full) {
-#pragma unroll
-        for (int it = 0; it < 16; ++it) { emit(v[it].x); emit(v[it].y); emit(v[it].z); emit(v[it].w); }
-    } else {
-        for (int64_t i = threadIdx.x; i < len; i += STREAM_THREADS) emit(p[i]);
-    }
-}
-
-/* --------------------------------------------------------------- k_select --- */
-constexpr int SEL_THREADS = 1024;
-
+/* --------------------------------------------------------- radix select --- */
 /* Find the digit (8 bits) holding rank r in a 256-bin LDS histogram; one wave. */
 __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, int* digit, int64_t* below) {
     const int lane = threadIdx.x & 63;
@@ -253,20 +94,22 @@ __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, i
     }
 }
 
-/* Radix select of ranks ra / rb (0-based) among keys produced by get(i), i < m, one block. */
-template <class Get>
-__device__ void block_radix_select2(const Get& get, int64_t m, int64_t ra, int64_t rb, bool need_a, bool need_b,
-                                    uint32_t* ka, uint32_t* kb) {
+/* Exact radix select (8-bit digits, MSB first) of ranks ra / rb (0-based, ascending) among
+ * the keys get(i), i < m, that satisfy keep(key); one block of THREADS threads. */
+template <int THREADS, class Get, class Keep>
+__device__ void block_radix_select2(const Get& get, const Keep& keep, int64_t m, int64_t ra, int64_t rb,
+                                    bool need_a, bool need_b, uint32_t* ka, uint32_t* kb) {
     __shared__ uint32_t ha[256], hb[256];
     __shared__ int dsel[2];
     __shared__ int64_t bsel[2];
     uint32_t pa = 0, pb = 0, mask = 0;
     for (int round = 0; round < 4; ++round) {
         const int shift = 24 - 8 * round;
-        for (int i = threadIdx.x; i < 256; i += SEL_THREADS) { ha[i] = 0; hb[i] = 0; }
+        for (int i = threadIdx.x; i < 256; i += THREADS) { ha[i] = 0; hb[i] = 0; }
         __syncthreads();
-        for (int64_t i = threadIdx.x; i < m; i += SEL_THREADS) {
+        for (int64_t i = threadIdx.x; i < m; i += THREADS) {
             const uint32_t k = get(i);
+            if (!keep(k)) continue;
             const uint32_t d = (k >> shift) & 255u;
             if (need_a && (k & mask) == pa) atomicAdd(&ha[d], 1u);
             if (need_b && (k & mask) == pb) atomicAdd(&hb[d], 1u);
@@ -285,27 +128,222 @@ __device__ void block_radix_select2(const Get& get, int64_t m, int64_t ra, int64
     *kb = pb;
 }
 
+/* --------------------------------------------------------------- k_sample --- */
+constexpr int SAMPLE_THREADS = 1024;
+
+__global__ __launch_bounds__(SAMPLE_THREADS) void k_sample(SegTable t, SelState* __restrict__ sel,
+                                                           wtp_result* __restrict__ res) {
+    __shared__ uint32_t sk[M_SAMPLE]; /* 128 KiB */
+    const SegDesc& sd = t.s[blockIdx.x];
+    const int64_t n = sd.n;
+    const bool exact = n <= M_SAMPLE;
+    const int m = exact ? (int)n : M_SAMPLE;
+    const float* x = sd.data;
+    if (exact) {
+        for (int i = threadIdx.x; i < m; i += SAMPLE_THREADS) sk[i] = abs_key(x[i]);
+    } else {
+        constexpr int G = M_SAMPLE / SAMPLE_GROUP;
+        for (int i = threadIdx.x; i < m; i += SAMPLE_THREADS) {
+            const int64_t g = i / SAMPLE_GROUP, j = i % SAMPLE_GROUP;
+            sk[i] = abs_key(x[g * (n - SAMPLE_GROUP) / (G - 1) + j]);
+        }
+    }
+    __syncthreads();
+    const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
+    int64_t sa, sb;
+    bool lo_open = false, hi_open = false;
+    if (exact) {
+        sa = r0;
+        sb = r1;
+    } else {
+        /* sample ranks bracketing r0 and r1 with a 6-sigma (+24) binomial margin */
+        const double p = (double)r0 / (double)(n - 1);
+        const double s0 = p * (double)(m - 1), s1 = (double)r1 / (double)(n - 1) * (double)(m - 1);
+        const double d = 6.0 * sqrt((double)m * p * (1.0 - p)) + 24.0;
+        sa = (int64_t)floor(s0 - d);
+        sb = (int64_t)ceil(s1 + d);
+        if (sa < 0) { lo_open = true; sa = 0; }
+        if (sb > m - 1) { hi_open = true; sb = m - 1; }
+    }
+    uint32_t ka, kb;
+    block_radix_select2<SAMPLE_THREADS>([&](int64_t i) { return sk[i]; }, [](uint32_t) { return true; }, m, sa, sb,
+                                        !lo_open, !hi_open, &ka, &kb);
+    if (threadIdx.x == 0) {
+        SelState& st = sel[sd.slot];
+        const uint32_t kl = lo_open ? 0u : ka;
+        const uint32_t kh = hi_open ? 0xFFFFFFFFu : kb;
+        st.kl = kl;
+        st.kh = kh;
+        uint32_t sh = 0;
+        if (kh > kl + 1) {
+            const uint32_t R = kh - kl - 1;
+            const int bits = 32 - __clz(R);
+            sh = bits > 8 ? bits - 8 : 0;
+        }
+        st.shift = sh;
+        res[sd.res].zero_count = 0;
+    }
+}
+
+/* -------------------------------------------------------------- k_collect --- */
+__global__ __launch_bounds__(STREAM_THREADS) void k_collect(SegTable t, SelState* __restrict__ sel,
+                                                            uint32_t* __restrict__ cand) {
+    __shared__ uint32_t lsub[NSUB];
+    __shared__ int wtot[STREAM_THREADS / 64];
+    __shared__ uint32_t sbase;
+    const int si = find_seg(t, blockIdx.x);
+    const SegDesc& sd = t.s[si];
+    const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * CHUNK;
+    const int64_t len = min((int64_t)CHUNK, sd.n - base);
+    const float* p = sd.data + base;
+    const bool full = (sd.flags & SEG_ALIGNED) && len == CHUNK;
+    float4 v[16];
+    if (full) load_chunk(p, v); /* issue the stream loads before the window state arrives */
+    SelState* st = sel + sd.slot;
+    const uint32_t kl = st->kl, kh = st->kh, sh = st->shift;
+    for (int i = threadIdx.x; i < NSUB; i += STREAM_THREADS) lsub[i] = 0;
+    __syncthreads();
+    uint32_t below = 0, eql = 0, eqh = 0, mx = 0;
+    int cnt = 0;
+    auto tally = [&](float xv) {
+        const uint32_t k = abs_key(xv);
+        mx = max(mx, k);
+        below += k < kl;
+        if (k == kl) ++eql;
+        else if (k == kh) ++eqh;
+        else if (k > kl && k < kh) { ++cnt; atomicAdd(&lsub[(k - kl - 1) >> sh], 1u); }
+    };
+    if (full) {
+#pragma unroll
+        for (int it = 0; it < 16; ++it) { tally(v[it].x); tally(v[it].y); tally(v[it].z); tally(v[it].w); }
+    } else {
+        for (int64_t i = threadIdx.x; i < len; i += STREAM_THREADS) tally(p[i]);
+    }
+    /* counters: one atomic per block each */
+    const unsigned long long tb = block_sum_u64<STREAM_THREADS>(below);
+    const unsigned long long tl = block_sum_u64<STREAM_THREADS>(eql);
+    const unsigned long long th = block_sum_u64<STREAM_THREADS>(eqh);
+    mx = wave_max_u32(mx);
+    if ((threadIdx.x & 63) == 0) atomicMax(&st->maxkey, mx);
+    if (threadIdx.x == 0) {
+        if (tb) atomicAdd(&st->below, tb);
+        if (tl) atomicAdd(&st->eq_lo, tl);
+        if (th) atomicAdd(&st->eq_hi, th);
+    }
+    /* inside keys: block exclusive scan, one returning atomic per block, then emit */
+    const int incl = (int)wave_incl_scan(cnt);
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 63) wtot[wv] = incl;
+    __syncthreads();
+    int off = incl - cnt, total = 0;
+    for (int i = 0; i < STREAM_THREADS / 64; ++i) {
+        if (i < wv) off += wtot[i];
+        total += wtot[i];
+    }
+    if (threadIdx.x == 0) sbase = total ? atomicAdd(&st->cand_count, (uint32_t)total) : 0u;
+    for (int i = threadIdx.x; i < NSUB; i += STREAM_THREADS) {
+        const uint32_t c = lsub[i];
+        if (c) atomicAdd(&st->sub[i], c);
+    }
+    __syncthreads();
+    if (!cnt) return;
+    const int64_t cap = sd.cap;
+    uint32_t* out = cand + sd.cand_off;
+    int64_t pos = (int64_t)sbase + off;
+    auto emit = [&](float xv) {
+        const uint32_t k = abs_key(xv);
+        if (k > kl && k < kh && k != kl && k != kh) {
+            if (pos < cap) out[pos] = k;
+            ++pos;
+        }
+    };
+    if (full) {
+#pragma unroll
+        for (int it = 0; it < 16; ++it) { emit(v[it].x); emit(v[it].y); emit(v[it].z); emit(v[it].w); }
+    } else {
+        for (int64_t i = threadIdx.x; i < len; i += STREAM_THREADS) emit(p[i]);
+    }
+}
+
+/* --------------------------------------------------------------- k_select --- */
+constexpr int SEL_THREADS = 1024;
+constexpr int SEL_STAGE = 16384; /* filtered candidates staged in LDS */
+
 __global__ __launch_bounds__(SEL_THREADS) void k_select(SegTable t, SelState* __restrict__ sel,
                                                         const uint32_t* __restrict__ cand,
-                                                        wtp_result* __restrict__ res) {
+                                                        wtp_result* __restrict__ res, float* __restrict__ thr_out) {
+    __shared__ uint32_t stage[SEL_STAGE];
+    __shared__ uint32_t nstage;
+    __shared__ int sbin[2];
+    __shared__ int64_t sbefore[2];
     const SegDesc& sd = t.s[blockIdx.x];
     SelState* st = sel + sd.slot;
-    const int mode = st->mode;
     const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
+    const int64_t below = (int64_t)st->below, eql = (int64_t)st->eq_lo, eqh = (int64_t)st->eq_hi;
+    const int64_t ncand = st->cand_count;
+    const uint32_t kl = st->kl, kh = st->kh, sh = st->shift;
+    /* class of a rank: 0 miss, 1 == kl, 2 inside, 3 == kh */
+    auto classify = [&](int64_t r, int64_t* j) {
+        if (r < below) return 0;
+        r -= below;
+        if (r < eql) return 1;
+        r -= eql;
+        if (r < ncand) { *j = r; return 2; }
+        r -= ncand;
+        if (r < eqh) return 3;
+        return 0;
+    };
+    int64_t ja = 0, jb = 0;
+    const int ca = classify(r0, &ja), cb = classify(r1, &jb);
     uint32_t ka = 0, kb = 0;
-    const bool need_a = !st->a_zero, need_b = !st->b_zero;
-    int path = MODE_ZERO;
-    if (mode == MODE_CAND) {
-        const uint32_t* c = cand + sd.cand_off;
-        const int64_t m = min((int64_t)st->cand_count, sd.cap);
-        const int64_t below = st->below;
-        block_radix_select2([&](int64_t i) { return c[i]; }, m, r0 - below, r1 - below, need_a, need_b, &ka, &kb);
-        path = MODE_CAND;
-    } else if (mode == MODE_FULL) {
+    int path;
+    if (ca == 0 || cb == 0 || ncand > sd.cap) {
+        /* the window missed (or overflowed): exact full radix select over the population */
         const float* x = sd.data;
-        block_radix_select2([&](int64_t i) { return abs_key(x[i]); }, sd.n, r0, r1, need_a, need_b, &ka, &kb);
+        block_radix_select2<SEL_THREADS>([&](int64_t i) { return abs_key(x[i]); }, [](uint32_t) { return true; },
+                                         sd.n, r0, r1, true, true, &ka, &kb);
         path = MODE_FULL;
+    } else {
+        ka = (ca == 1) ? kl : kh;
+        kb = (cb == 1) ? kl : kh;
+        path = MODE_WINDOW;
+        if (ca == 2 || cb == 2) {
+            path = MODE_CAND;
+            /* sub-bins holding the inside ranks (bins between two adjacent ranks are empty) */
+            if (threadIdx.x < 64) {
+                if (ca == 2) wave_pick_digit(st->sub, ja, &sbin[0], &sbefore[0]);
+                if (cb == 2) wave_pick_digit(st->sub, jb, &sbin[1], &sbefore[1]);
+            }
+            if (threadIdx.x == 0) nstage = 0;
+            __syncthreads();
+            const int blo = (ca == 2) ? sbin[0] : sbin[1];
+            const int bhi = (cb == 2) ? sbin[1] : sbin[0];
+            const int64_t before = (ca == 2) ? sbefore[0] : sbefore[1];
+            int64_t nf = 0;
+            for (int b = blo; b <= bhi; ++b) nf += st->sub[b];
+            const uint32_t* c = cand + sd.cand_off;
+            auto keep = [&](uint32_t k) {
+                const int b = (int)((k - kl - 1) >> sh);
+                return b >= blo && b <= bhi;
+            };
+            uint32_t xa, xb;
+            if (nf <= SEL_STAGE) {
+                for (int64_t i = threadIdx.x; i < ncand; i += SEL_THREADS) {
+                    const uint32_t k = c[i];
+                    if (keep(k)) stage[atomicAdd(&nstage, 1u)] = k;
+                }
+                __syncthreads();
+                block_radix_select2<SEL_THREADS>([&](int64_t i) { return stage[i]; }, [](uint32_t) { return true; },
+                                                 (int64_t)nstage, ja - before, jb - before, ca == 2, cb == 2, &xa, &xb);
+            } else {
+                block_radix_select2<SEL_THREADS>([&](int64_t i) { return c[i]; }, keep, ncand, ja - before,
+                                                 jb - before, ca == 2, cb == 2, &xa, &xb);
+            }
+            if (ca == 2) ka = xa;
+            if (cb == 2) kb = xb;
+        }
     }
+    __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t mk = st->maxkey;
         const float fa = __uint_as_float(ka), fb = __uint_as_float(kb);
@@ -316,10 +354,16 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(SegTable t, SelState* __
         if (mk > 0x7F800000u) thr = __longlong_as_double(0x7FF8000000000000ll); /* NaN present */
         const float thr32 = (float)thr;
         st->thr32 = thr32;
+        thr_out[sd.res] = thr32; /* per tensor, read by the inverse transform */
         st->key_a = ka;
         st->key_b = kb;
-        st->cand_count = 0; /* leave the slot clean for the next call */
+        st->mode = path;
+        /* leave the slot clean for the next call */
+        st->cand_count = 0;
         st->maxkey = 0;
+        st->below = 0;
+        st->eq_lo = 0;
+        st->eq_hi = 0;
         wtp_result& r = res[sd.res];
         r.numel = sd.numel;
         r.coeff_numel = sd.n;
@@ -329,6 +373,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(SegTable t, SelState* __
         r.eff_level = sd.eff_level;
         r.path = path;
     }
+    for (int i = threadIdx.x; i < NSUB; i += SEL_THREADS) st->sub[i] = 0;
 }
 
 /* ----------------------------------------------------------------- k_mask --- */
@@ -497,17 +542,15 @@ static inline unsigned grid_for(int64_t total) {
     return (unsigned)g;
 }
 
-void launch_hist(const SegTable& t, uint32_t* hist, SelState* sel, hipStream_t s) {
-    hipLaunchKernelGGL(k_hist, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, hist, sel);
+void launch_sample(const SegTable& t, SelState* sel, wtp_result* res, hipStream_t s) {
+    hipLaunchKernelGGL(k_sample, dim3(t.nseg), dim3(SAMPLE_THREADS), 0, s, t, sel, res);
 }
-void launch_findbin(const SegTable& t, uint32_t* hist, SelState* sel, wtp_result* res, hipStream_t s) {
-    hipLaunchKernelGGL(k_findbin, dim3(t.nseg), dim3(FB_THREADS), 0, s, t, hist, sel, res);
+void launch_collect(const SegTable& t, SelState* sel, uint32_t* cand, hipStream_t s) {
+    hipLaunchKernelGGL(k_collect, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, sel, cand);
 }
-void launch_compact(const SegTable& t, SelState* sel, uint32_t* cand, hipStream_t s) {
-    hipLaunchKernelGGL(k_compact, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, sel, cand);
-}
-void launch_select(const SegTable& t, SelState* sel, const uint32_t* cand, wtp_result* res, hipStream_t s) {
-    hipLaunchKernelGGL(k_select, dim3(t.nseg), dim3(SEL_THREADS), 0, s, t, sel, cand, res);
+void launch_select(const SegTable& t, SelState* sel, const uint32_t* cand, wtp_result* res, float* thr_out,
+                   hipStream_t s) {
+    hipLaunchKernelGGL(k_select, dim3(t.nseg), dim3(SEL_THREADS), 0, s, t, sel, cand, res, thr_out);
 }
 void launch_mask(const SegTable& t, const SelState* sel, wtp_result* res, hipStream_t s) {
     hipLaunchKernelGGL(k_mask, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, sel, res);

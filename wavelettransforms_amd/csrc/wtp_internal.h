@@ -12,27 +12,15 @@
 
 namespace wtp {
 
-/* ---- selection histogram: bins over the float32 bit pattern of |x| (monotone in |x|) ----
- * bin 0        : exact zeros (+0/-0)
- * bin 1        : 0 < |x| < 2^(WIN_E0-127)               (below the window)
- * bins 2..     : exponent window [WIN_E0, WIN_E0+WIN_EXP) x 2^MANT_BITS mantissa slices
- * bin NB-1     : |x| >= 2^(WIN_E0+WIN_EXP-127), inf, NaN
- * 1/128-octave slices keep the population of the bin holding the percentile at ~0.3-1% of a
- * weight tensor, which the candidate pass gathers and the select kernel resolves exactly. */
-constexpr int WIN_EXP = 32;
-constexpr int MANT_BITS = 7;
-constexpr uint32_t WIN_E0 = 101; /* window = [2^-26, 2^6) */
-constexpr int NB = 3 + (WIN_EXP << MANT_BITS); /* 4099 */
-constexpr int BIN_ZERO = 0, BIN_UNDER = 1, BIN_OVER = NB - 1;
-constexpr int NB_PAD = 4112; /* per-slot stride (16-word multiple) */
-
-__host__ __device__ __forceinline__ int key_bin(uint32_t key) {
-    if (key == 0) return BIN_ZERO;
-    const uint32_t e = key >> 23;
-    if (e < WIN_E0) return BIN_UNDER;
-    if (e >= WIN_E0 + WIN_EXP) return BIN_OVER;
-    return 2 + (int)(((e - WIN_E0) << MANT_BITS) | ((key >> (23 - MANT_BITS)) & ((1u << MANT_BITS) - 1)));
-}
+/* ---- selection: sample window + one counting/collecting pass ----
+ * k_sample brackets the two order statistics r0, r0+1 of |x| with a window [kl, kh] taken
+ * from M_SAMPLE sampled keys (the exact values when the population fits in the sample);
+ * k_collect streams the data once, counting keys below kl / equal to kl / equal to kh and
+ * gathering the keys strictly inside (kl, kh) with a 256-bin sub-histogram; k_select
+ * resolves both ranks exactly (or, if the window missed, by a full radix select). */
+constexpr int M_SAMPLE = 32768;
+constexpr int SAMPLE_GROUP = 16;   /* contiguous keys per sample group */
+constexpr int NSUB = 256;          /* sub-histogram bins over (kl, kh) */
 
 /* ---- grouped launches over segments (one segment = one selection population) ---- */
 constexpr int CHUNK = 16384;        /* elements per block in the streaming passes */
@@ -68,22 +56,27 @@ struct SegTable {
     SegDesc s[SEG_PER_LAUNCH];
 };
 
-/* per-slot selection state (workspace, zeroed once, left zeroed by every call) */
+/* per-slot selection state.  Slots are the positions of a segment inside its launch group
+ * (0..SEG_PER_LAUNCH-1); the SelState slots sit at the very start of every workspace
+ * layout, so every call sees the same persistent region: zeroed once by wtp_workspace_init
+ * and left zeroed (counters) by every call -- k_select clears what k_collect accumulated. */
 struct SelState {
-    uint32_t maxkey;     /* atomicMax in k_hist; reset by k_select              */
-    uint32_t cand_count; /* atomicAdd in k_compact; reset by k_select           */
-    uint32_t cb_lo;      /* candidate bin range [cb_lo, cb_hi]                  */
-    uint32_t cb_hi;
-    int64_t below;       /* population in bins < cb_lo                          */
-    int32_t mode;        /* MODE_*                                              */
-    uint32_t key_a;      /* resolved order statistics (bit patterns of |x|)     */
-    uint32_t key_b;
-    float thr32;         /* the float32 threshold the compare uses              */
-    int32_t a_zero;      /* lower statistic sits in the zero bin                */
-    int32_t b_zero;
+    uint32_t maxkey;             /* atomicMax (k_collect)                                 */
+    uint32_t cand_count;         /* atomicAdd (k_collect): keys strictly inside (kl, kh)  */
+    unsigned long long below;    /* atomicAdd (k_collect): keys < kl                       */
+    unsigned long long eq_lo;    /* keys == kl                                            */
+    unsigned long long eq_hi;    /* keys == kh (kh != kl)                                 */
+    uint32_t kl, kh;             /* window (k_sample); kh = 0xFFFFFFFF: unbounded          */
+    uint32_t shift;              /* sub-bin of an inside key = (key - kl - 1) >> shift     */
+    int32_t mode;                /* MODE_* chosen by k_select (diagnostics)                */
+    float thr32;                 /* the float32 threshold the compare uses                 */
+    uint32_t key_a, key_b;       /* resolved order statistics                              */
+    uint32_t pad[1];
+    uint32_t sub[NSUB];          /* sub-histogram of inside keys (atomicAdd, k_collect)    */
 };
+static_assert(sizeof(SelState) % 64 == 0, "SelState padding");
 
-enum SelMode : int32_t { MODE_CAND = 1, MODE_ZERO = 2, MODE_FULL = 3 };
+enum SelMode : int32_t { MODE_CAND = 1, MODE_WINDOW = 2, MODE_FULL = 3 };
 
 /* filter taps as a kernel argument (scalar-loaded, uniform across the wave) */
 struct Taps {
@@ -93,10 +86,10 @@ struct Taps {
 };
 
 /* ---- launchers (kernels.hip) ---- */
-void launch_hist(const SegTable& t, uint32_t* hist, SelState* sel, hipStream_t s);
-void launch_findbin(const SegTable& t, uint32_t* hist, SelState* sel, wtp_result* res, hipStream_t s);
-void launch_compact(const SegTable& t, SelState* sel, uint32_t* cand, hipStream_t s);
-void launch_select(const SegTable& t, SelState* sel, const uint32_t* cand, wtp_result* res, hipStream_t s);
+void launch_sample(const SegTable& t, SelState* sel, wtp_result* res, hipStream_t s);
+void launch_collect(const SegTable& t, SelState* sel, uint32_t* cand, hipStream_t s);
+void launch_select(const SegTable& t, SelState* sel, const uint32_t* cand, wtp_result* res, float* thr_out,
+                   hipStream_t s);
 void launch_mask(const SegTable& t, const SelState* sel, wtp_result* res, hipStream_t s);
 
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
