@@ -114,12 +114,12 @@ def test_batched_resnet18_equals_oracle_per_layer(eng):
 def test_window_miss_falls_back_to_full_scan(eng):
     """Data whose sampled positions are unrepresentative: the sample window misses the true
     order statistics and k_select must fall back to the exact full radix select (path 3)."""
-    n, G, grp = 300_000, 32768 // 16, 16
+    n, ng, grp = 300_000, 32768 // 16, 16
     x = np.full(n, 2.0, np.float32)
     rng = np.random.default_rng(3)
     x += rng.integers(0, 1 << 12, n).astype(np.float32) * np.float32(2.0 ** -20)
-    for g in range(G):
-        s = g * (n - grp) // (G - 1)
+    for g in range(ng):
+        s = g * (n - grp) // (ng - 1)
         x[s:s + grp] = 1.0
     x[::7] *= -1
     outs, (r,) = eng.prune([_dev(x).reshape(300, 1000)], "bior3.3", 0, 37.5)   # level 0: raw values

@@ -89,12 +89,24 @@ constexpr size_t PERSIST_BYTES = ((SEG_PER_LAUNCH * sizeof(SelState)) + 255) / 2
 
 bool pct_ok(double pct) { return pct >= 0.0 && pct <= 100.0; }
 
+/* candidate buckets: the sample window holds ~3.6% of a large population (6-sigma margins at
+ * 32768 samples); size the bucket count for ~1000 expected keys each and give every bucket
+ * ~4x headroom (an overflowing bucket sends k_select to its exact full-scan path). */
+void bucket_plan(int64_t n, int* nsub_log2, int* bucket_cap) {
+    const double expect = 0.05 * (double)n;
+    int lg = 6;
+    while (lg < 10 && (double)(1 << lg) * 1024.0 < expect) ++lg;
+    int64_t bc = (int64_t)(4.0 * expect / (double)(1 << lg)) + 1;
+    if (bc < 256) bc = 256;
+    if (bc > BUCKET_MAX) bc = BUCKET_MAX;
+    *nsub_log2 = lg;
+    *bucket_cap = (int)bc;
+}
+
 int64_t cap_for(int64_t n) {
-    /* the sample window holds ~3-4% of a large population (6-sigma margins at 32768 samples) */
-    int64_t c = (n + 7) / 8;
-    if (c < 65536) c = 65536;
-    if (c > n) c = n;
-    return (c + 63) / 64 * 64;
+    int lg, bc;
+    bucket_plan(n, &lg, &bc);
+    return (int64_t)bc << lg;
 }
 
 /* Validate and plan every tensor in the reference's order; returns WTP_OK or the first error. */
@@ -333,6 +345,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             seg_ranks(p.pop, pct, sd);
             sd.numel = p.numel;
             sd.blk_begin = blk;
+            tab.blk_begin[tab.nseg - 1] = blk;
             sd.slot = t - g0;
             sd.res = t;
             sd.eff_level = p.L;
@@ -341,18 +354,20 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             if ((a % 16) == 0 && (o % 16) == 0) sd.flags |= SEG_ALIGNED;
             sd.cand_off = (int64_t)p.cand_off;
             sd.cap = p.cap;
+            bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap);
             blk += (int)((p.pop + CHUNK - 1) / CHUNK);
         }
         tab.nblk = blk;
+        for (int i = tab.nseg; i < SEG_PER_LAUNCH; ++i) tab.blk_begin[i] = INT32_MAX;
         const bool first = g0 == 0;
         if (first) stage(1, s);
-        launch_sample(tab, sel, results, s);
+        launch_sample(tab, sel, s);
         if (first) stage(2, s);
         launch_collect(tab, sel, cand, s);
         if (first) stage(3, s);
         launch_select(tab, sel, cand, results, thr_t, s);
         if (first) stage(4, s);
-        launch_mask(tab, sel, results, s);
+        launch_mask(tab, thr_t, s);
         if (first) stage(5, s);
     }
     /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2) */

@@ -13,14 +13,40 @@
 namespace wtp {
 
 /* ---- selection: sample window + one counting/collecting pass ----
- * k_sample brackets the two order statistics r0, r0+1 of |x| with a window [kl, kh] taken
- * from M_SAMPLE sampled keys (the exact values when the population fits in the sample);
- * k_collect streams the data once, counting keys below kl / equal to kl / equal to kh and
- * gathering the keys strictly inside (kl, kh) with a 256-bin sub-histogram; k_select
- * resolves both ranks exactly (or, if the window missed, by a full radix select). */
+ * k_sample histograms M_SAMPLE sampled keys (the whole segment when it fits) into 4099 bins
+ * of the float32 bit pattern of |x| (1/128 octave in [2^-26, 2^6), plus zero / under /
+ * over bins) and sets a window [kl, kh] of bin edges that brackets the order statistics
+ * r0, r0+1 with a 6-sigma binomial margin; k_collect streams the data once, counting keys
+ * < kl, == kl, == kh and == 0 and scattering the keys strictly inside (kl, kh) into nsub
+ * key-range buckets; k_select reads only the bucket(s) holding the two ranks and resolves
+ * them exactly, or by a full radix select over the segment if the window missed. */
 constexpr int M_SAMPLE = 32768;
 constexpr int SAMPLE_GROUP = 16;   /* contiguous keys per sample group */
-constexpr int NSUB = 256;          /* sub-histogram bins over (kl, kh) */
+constexpr int NSUB_MAX = 1024;     /* buckets over (kl, kh): 64..1024 per segment (SegDesc) */
+constexpr int BUCKET_MAX = 8192;   /* keys per bucket (two buckets are staged in LDS)       */
+constexpr int WIN_EXP = 32;
+constexpr int MANT_BITS = 7;
+constexpr uint32_t WIN_E0 = 101;   /* bin window = [2^-26, 2^6) */
+constexpr int NB = 3 + (WIN_EXP << MANT_BITS); /* 4099 */
+constexpr int BIN_ZERO = 0, BIN_UNDER = 1, BIN_OVER = NB - 1;
+
+__host__ __device__ __forceinline__ int key_bin(uint32_t key) {
+    if (key == 0) return BIN_ZERO;
+    const uint32_t e = key >> 23;
+    if (e < WIN_E0) return BIN_UNDER;
+    if (e >= WIN_E0 + WIN_EXP) return BIN_OVER;
+    return 2 + (int)(((e - WIN_E0) << MANT_BITS) | ((key >> (23 - MANT_BITS)) & ((1u << MANT_BITS) - 1)));
+}
+/* smallest key of bin b, and the smallest key of the bins above b */
+__host__ __device__ __forceinline__ uint32_t bin_lo_key(int b) {
+    if (b <= BIN_ZERO) return 0u;
+    if (b == BIN_UNDER) return 1u;
+    if (b == BIN_OVER) return (WIN_E0 + WIN_EXP) << 23;
+    return ((WIN_E0 + ((uint32_t)(b - 2) >> MANT_BITS)) << 23) | (((uint32_t)(b - 2) & ((1u << MANT_BITS) - 1)) << (23 - MANT_BITS));
+}
+__host__ __device__ __forceinline__ uint32_t bin_hi_key(int b) { /* exclusive; 0xFFFFFFFF = unbounded */
+    return b >= BIN_OVER ? 0xFFFFFFFFu : bin_lo_key(b + 1);
+}
 
 /* ---- grouped launches over segments (one segment = one selection population) ---- */
 constexpr int CHUNK = 16384;        /* elements per block in the streaming passes */
@@ -45,14 +71,17 @@ struct SegDesc {
     int32_t flags;
     int32_t eff_level;
     int32_t above;     /* vi >= n-1: both order statistics are the maximum               */
-    int64_t cand_off;  /* this segment's candidate buffer (elements into the workspace)  */
-    int64_t cap;       /* its capacity                                                   */
+    int64_t cand_off;  /* this segment's candidate buckets (elements into the workspace) */
+    int64_t cap;       /* nsub * bucket_cap                                              */
+    int32_t nsub_log2; /* 6..10                                                          */
+    int32_t bucket_cap;
 };
 
 struct SegTable {
     int32_t nseg;
     int32_t nblk;
     int32_t pad[2];
+    int32_t blk_begin[SEG_PER_LAUNCH]; /* INT32_MAX past nseg: block -> segment in one scalar sweep */
     SegDesc s[SEG_PER_LAUNCH];
 };
 
@@ -62,17 +91,18 @@ struct SegTable {
  * and left zeroed (counters) by every call -- k_select clears what k_collect accumulated. */
 struct SelState {
     uint32_t maxkey;             /* atomicMax (k_collect)                                 */
-    uint32_t cand_count;         /* atomicAdd (k_collect): keys strictly inside (kl, kh)  */
+    uint32_t overflow;           /* a block had more inside keys than it can stage        */
     unsigned long long below;    /* atomicAdd (k_collect): keys < kl                       */
     unsigned long long eq_lo;    /* keys == kl                                            */
     unsigned long long eq_hi;    /* keys == kh (kh != kl)                                 */
+    unsigned long long zeros;    /* keys == 0                                             */
     uint32_t kl, kh;             /* window (k_sample); kh = 0xFFFFFFFF: unbounded          */
-    uint32_t shift;              /* sub-bin of an inside key = (key - kl - 1) >> shift     */
+    uint32_t shift;              /* bucket of an inside key = (key - kl - 1) >> shift      */
     int32_t mode;                /* MODE_* chosen by k_select (diagnostics)                */
     float thr32;                 /* the float32 threshold the compare uses                 */
     uint32_t key_a, key_b;       /* resolved order statistics                              */
-    uint32_t pad[1];
-    uint32_t sub[NSUB];          /* sub-histogram of inside keys (atomicAdd, k_collect)    */
+    uint32_t pad[15];
+    uint32_t sub[NSUB_MAX];      /* keys per bucket (returning atomicAdd, k_collect)       */
 };
 static_assert(sizeof(SelState) % 64 == 0, "SelState padding");
 
@@ -86,11 +116,11 @@ struct Taps {
 };
 
 /* ---- launchers (kernels.hip) ---- */
-void launch_sample(const SegTable& t, SelState* sel, wtp_result* res, hipStream_t s);
+void launch_sample(const SegTable& t, SelState* sel, hipStream_t s);
 void launch_collect(const SegTable& t, SelState* sel, uint32_t* cand, hipStream_t s);
 void launch_select(const SegTable& t, SelState* sel, const uint32_t* cand, wtp_result* res, float* thr_out,
                    hipStream_t s);
-void launch_mask(const SegTable& t, const SelState* sel, wtp_result* res, hipStream_t s);
+void launch_mask(const SegTable& t, const float* thr, hipStream_t s);
 
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
                      hipStream_t s);
