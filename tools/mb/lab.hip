@@ -1,6 +1,9 @@
 // Kernel lab: times each selection kernel of libwtprune in isolation on the cfg2 footprint
 // (20 separately allocated ResNet-18 conv tensors), plus reference copy/read kernels.
 // Not part of the product.  Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off lab.hip
+#include <hip/hip_runtime.h>
+__device__ unsigned long long g_probe[24][8];
+#define WTP_PROBE(i) do { if (threadIdx.x == 0) g_probe[blockIdx.x][i] = wall_clock64(); } while (0)
 #include "../../wavelettransforms_amd/csrc/kernels.hip"
 #include <cstdio>
 #include <cstring>
@@ -9,6 +12,13 @@
 #include <cmath>
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 using namespace wtp;
+
+__global__ void k_dpp_test(const uint32_t* in, uint32_t* scan, uint32_t* mx, unsigned long long* sum64) {
+    const uint32_t v = in[blockIdx.x * 256 + threadIdx.x];
+    scan[blockIdx.x * 256 + threadIdx.x] = wave_scan_u32(v);
+    mx[blockIdx.x * 256 + threadIdx.x] = wave_max_u32(v);
+    sum64[blockIdx.x * 256 + threadIdx.x] = wave_sum_u64(((unsigned long long)v << 20) ^ v);
+}
 
 __global__ void k_copy16(const float4* __restrict__ p, float4* __restrict__ q, int64_t n4, float thr) {
     int64_t base = (int64_t)blockIdx.x * 256 * 16;
@@ -58,7 +68,7 @@ __global__ __launch_bounds__(256) void k_maskv(SegTable t, const SelState* __res
     auto f = [&](float x) { const float y = (fabsf(x) < thr) ? 0.0f : x; z += (y == 0.0f); return y; };
     if (len == CHUNK) {
         float4 v[16];
-        load_chunk(p, v);
+        load_chunk<16>(p, v);
         float4* q4 = reinterpret_cast<float4*>(q);
 #pragma unroll
         for (int it = 0; it < 16; ++it) {
@@ -75,6 +85,27 @@ __global__ __launch_bounds__(256) void k_maskv(SegTable t, const SelState* __res
 }
 
 int main() {
+    {   // DPP wave primitives vs serial
+        const int N = 4096;
+        std::vector<uint32_t> h(N); uint64_t z = 88172645463325252ull;
+        for (auto& v : h) { z ^= z << 13; z ^= z >> 7; z ^= z << 17; v = (uint32_t)(z >> ((z & 3) * 8)); }
+        uint32_t *din, *dsc, *dmx; unsigned long long* ds64;
+        CK(hipMalloc(&din, N * 4)); CK(hipMalloc(&dsc, N * 4)); CK(hipMalloc(&dmx, N * 4)); CK(hipMalloc(&ds64, N * 8));
+        CK(hipMemcpy(din, h.data(), N * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_dpp_test, dim3(N / 256), dim3(256), 0, 0, din, dsc, dmx, ds64);
+        std::vector<uint32_t> sc(N), mx(N); std::vector<unsigned long long> s64(N);
+        CK(hipMemcpy(sc.data(), dsc, N * 4, hipMemcpyDeviceToHost)); CK(hipMemcpy(mx.data(), dmx, N * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(s64.data(), ds64, N * 8, hipMemcpyDeviceToHost));
+        int bad = 0;
+        for (int w = 0; w < N / 64; ++w) {
+            uint32_t acc = 0, m = 0; unsigned long long a64 = 0;
+            for (int l = 0; l < 64; ++l) { m = std::max(m, h[w * 64 + l]); a64 += ((unsigned long long)h[w * 64 + l] << 20) ^ h[w * 64 + l]; }
+            for (int l = 0; l < 64; ++l) { acc += h[w * 64 + l]; bad += sc[w * 64 + l] != acc; bad += mx[w * 64 + l] != m; bad += s64[w * 64 + l] != a64; }
+        }
+        printf("DPP primitives: %d mismatches\n", bad);
+        if (bad) return 1;
+    }
+
     const int shapes[20] = {9408, 36864, 36864, 36864, 36864, 8192, 73728, 147456, 147456, 147456, 32768, 294912,
                             589824, 589824, 589824, 131072, 1179648, 2359296, 2359296, 2359296};
     std::vector<float*> xs(20), ys(20);
@@ -118,55 +149,98 @@ int main() {
     };
     // full pipeline once to get state
     for (int i = t.nseg; i < SEG_PER_LAUNCH; ++i) t.blk_begin[i] = INT32_MAX;
-    auto pipeline = [&]{ launch_sample(t, sel, 0); launch_collect(t, sel, cand, 0); launch_select(t, sel, cand, res, thr, 0); launch_mask(t, thr, 0); };
-    bench("pipeline (4 kernels)", pipeline, tot * 8.0);
+    auto pipeline = [&]{ launch_sample(t, sel, 0); launch_collect_select(t, sel, cand, res, thr, 0); launch_mask(t, thr, res, 0); };
+    bench("pipeline (3 kernels)", pipeline, tot * 8.0);
     bench("copy16 contiguous", [&]{ hipLaunchKernelGGL(k_copy16, dim3((tot/4 + 4095)/4096), dim3(256), 0, 0, (float4*)cx, (float4*)cy, tot/4, 0.01f); }, tot * 8.0);
-    bench("k_mask", [&]{ launch_mask(t, thr, 0); }, tot * 8.0);
+    bench("k_mask", [&]{ launch_mask(t, thr, res, 0); }, tot * 8.0);
     const int fb = (int)(tot / CHUNK);
 #define V(S, G, Z, B, nm) bench(nm, [&]{ hipLaunchKernelGGL((k_maskv<S, G, Z, B>), dim3(S ? t.nblk : fb), dim3(256), 0, 0, t, sel, res, cx, cy, 0.0015f); }, tot * 8.0);
     V(false, false, false, false, "maskv flat")
-    V(false, false, true, false, "maskv flat +zc")
     V(true, false, false, false, "maskv seg")
-    V(true, false, false, true, "maskv seg blktab")
-    V(true, true, false, false, "maskv seg +thrg")
     V(true, true, true, false, "maskv seg +thrg +zc")
-    V(true, true, true, true, "maskv seg blktab +thrg +zc")
     bench("k_sample", [&]{ launch_sample(t, sel, 0); }, 0);
-    // collect + select must stay paired (select resets the counters)
-    bench("k_collect+k_select", [&]{ launch_collect(t, sel, cand, 0); launch_select(t, sel, cand, res, thr, 0); }, tot * 4.0);
+    bench("k_sample_t<4096>", [&]{ hipLaunchKernelGGL(k_sample_t<4096>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }, 0);
+    bench("k_sample_t<16384>", [&]{ hipLaunchKernelGGL(k_sample_t<16384>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }, 0);
+    {   // pipelines with different sample sizes
+        auto pipe = [&](auto ks) { ks(); launch_collect_select(t, sel, cand, res, thr, 0); launch_mask(t, thr, res, 0); };
+        bench("pipeline MS=4096", [&]{ pipe([&]{ hipLaunchKernelGGL(k_sample_t<4096>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }); }, tot * 8.0);
+        bench("pipeline MS=16384", [&]{ pipe([&]{ hipLaunchKernelGGL(k_sample_t<16384>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }); }, tot * 8.0);
+        std::vector<wtp_result> r1(20), r2(20);
+        pipe([&]{ hipLaunchKernelGGL(k_sample_t<4096>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }); CK(hipDeviceSynchronize());
+        CK(hipMemcpy(r1.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
+        pipe([&]{ hipLaunchKernelGGL(k_sample_t<32768>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }); CK(hipDeviceSynchronize());
+        CK(hipMemcpy(r2.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
+        int bad = 0; for (int i = 0; i < 20; ++i) bad += r1[i].thr64 != r2[i].thr64 || r1[i].zero_count != r2[i].zero_count || r1[i].path == 3;
+        printf("MS=4096 vs 32768 mismatches/fallbacks: %d\n", bad);
+    }
+    {   // collect ablations (counters accumulate: the state is re-zeroed after)
+        bench("collect LAB1 counters only", [&]{ hipLaunchKernelGGL((k_collect_t<1, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
+        bench("collect LAB2 +staging", [&]{ hipLaunchKernelGGL((k_collect_t<2, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
+        CK(hipMemset(sel, 0, selb)); launch_sample(t, sel, 0); CK(hipDeviceSynchronize());
+    }
+    bench("k_collect+k_select", [&]{ launch_collect_select(t, sel, cand, res, thr, 0); }, tot * 4.0);
+    {   // items per thread in k_collect: pipeline time and results vs the production IT
+        std::vector<wtp_result> r0(20), r1(20);
+        pipeline(); CK(hipDeviceSynchronize());
+        CK(hipMemcpy(r0.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
+        auto run_it = [&](const char* nm, int it, auto kc) {
+            auto pipe = [&] { launch_sample(t, sel, 0); kc(); hipLaunchKernelGGL(k_select, dim3(t.nseg), dim3(SEL_THREADS), 0, 0, t, sel, cand, res, thr); launch_mask(t, thr, res, 0); };
+            char b1[64]; snprintf(b1, 64, "pipeline IT=%d", it); bench(b1, pipe, tot * 8.0);
+            char b2[64]; snprintf(b2, 64, "collect+select IT=%d", it);
+            bench(b2, [&] { kc(); hipLaunchKernelGGL(k_select, dim3(t.nseg), dim3(SEL_THREADS), 0, 0, t, sel, cand, res, thr); }, tot * 4.0);
+            pipe(); CK(hipDeviceSynchronize());
+            CK(hipMemcpy(r1.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
+            int bad = 0; for (int i = 0; i < 20; ++i) bad += r0[i].thr64 != r1[i].thr64 || r0[i].zero_count != r1[i].zero_count || r1[i].path == 3;
+            printf("  %s: mismatches/fallbacks vs production %d\n", nm, bad);
+        };
+        run_it("IT4", 4, [&] { hipLaunchKernelGGL((k_collect_t<0, 4>), dim3(t.nblk * 4), dim3(256), 0, 0, t, sel, cand); });
+        run_it("IT8", 8, [&] { hipLaunchKernelGGL((k_collect_t<0, 8>), dim3(t.nblk * 2), dim3(256), 0, 0, t, sel, cand); });
+        run_it("IT16", 16, [&] { hipLaunchKernelGGL((k_collect_t<0, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); });
+        // collect alone (counters accumulate; re-zeroed after)
+        bench("collect IT4 alone", [&] { hipLaunchKernelGGL((k_collect_t<0, 4>), dim3(t.nblk * 4), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
+        bench("collect IT8 alone", [&] { hipLaunchKernelGGL((k_collect_t<0, 8>), dim3(t.nblk * 2), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
+        bench("collect IT16 alone", [&] { hipLaunchKernelGGL((k_collect_t<0, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
+        bench("collect IT4 LAB1", [&] { hipLaunchKernelGGL((k_collect_t<1, 4>), dim3(t.nblk * 4), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
+        bench("collect IT4 LAB2", [&] { hipLaunchKernelGGL((k_collect_t<2, 4>), dim3(t.nblk * 4), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
+        CK(hipMemset(sel, 0, selb)); CK(hipMemset(cand, 0, 4)); launch_sample(t, sel, 0); CK(hipDeviceSynchronize());
+    }
     {
-        // per-stage times of the real sequence (events between the kernels, queue pre-filled)
-        hipEvent_t ev[5]; for (auto& evx : ev) CK(hipEventCreate(&evx));
+        // per-stage times of the real sequence (events between the kernels)
+        hipEvent_t ev[4]; for (auto& evx : ev) CK(hipEventCreate(&evx));
         float* big; CK(hipMalloc(&big, 256 << 20));
-        double acc[4] = {0, 0, 0, 0};
-        const int R = 20;
-        for (int r = 0; r < R; ++r) {
-            CK(hipMemsetAsync(big, r, 256 << 20));
-            CK(hipEventRecord(ev[0])); launch_sample(t, sel, 0);
-            CK(hipEventRecord(ev[1])); launch_collect(t, sel, cand, 0);
-            CK(hipEventRecord(ev[2])); launch_select(t, sel, cand, res, thr, 0);
-            CK(hipEventRecord(ev[3])); launch_mask(t, thr, 0);
-            CK(hipEventRecord(ev[4])); CK(hipEventSynchronize(ev[4]));
-            for (int i = 0; i < 4; ++i) { float ms; CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1])); acc[i] += ms * 1e3; }
+        for (int mode = 0; mode < 2; ++mode) {
+            double acc[3] = {0, 0, 0};
+            const int R = 20;
+            for (int r = 0; r < R; ++r) {
+                if (mode == 0) CK(hipMemsetAsync(big, r, 256 << 20));
+                else hipLaunchKernelGGL(k_copy16, dim3((tot/4 + 4095)/4096), dim3(256), 0, 0, (float4*)cx, (float4*)cy, tot/4, 0.01f);
+                CK(hipEventRecord(ev[0])); launch_sample(t, sel, 0);
+                CK(hipEventRecord(ev[1])); launch_collect_select(t, sel, cand, res, thr, 0);
+                CK(hipEventRecord(ev[2])); launch_mask(t, thr, res, 0);
+                CK(hipEventRecord(ev[3])); CK(hipEventSynchronize(ev[3]));
+                for (int i = 0; i < 3; ++i) { float ms; CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1])); acc[i] += ms * 1e3; }
+            }
+            printf("stages (%s): sample %.2f collect+select %.2f mask %.2f us\n", mode ? "warm" : "after 256MB memset", acc[0]/R, acc[1]/R, acc[2]/R);
         }
-        printf("stages (after 256MB memset): sample %.2f collect %.2f select %.2f mask %.2f us\n", acc[0]/R, acc[1]/R, acc[2]/R, acc[3]/R);
-        for (int i = 0; i < 4; ++i) acc[i] = 0;
-        for (int r = 0; r < R; ++r) {
-            hipLaunchKernelGGL(k_copy16, dim3((tot/4 + 4095)/4096), dim3(256), 0, 0, (float4*)cx, (float4*)cy, tot/4, 0.01f);
-            CK(hipEventRecord(ev[0])); launch_sample(t, sel, 0);
-            CK(hipEventRecord(ev[1])); launch_collect(t, sel, cand, 0);
-            CK(hipEventRecord(ev[2])); launch_select(t, sel, cand, res, thr, 0);
-            CK(hipEventRecord(ev[3])); launch_mask(t, thr, 0);
-            CK(hipEventRecord(ev[4])); CK(hipEventSynchronize(ev[4]));
-            for (int i = 0; i < 4; ++i) { float ms; CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1])); acc[i] += ms * 1e3; }
-        }
-        printf("stages (warm): sample %.2f collect %.2f select %.2f mask %.2f us\n", acc[0]/R, acc[1]/R, acc[2]/R, acc[3]/R);
         std::vector<SelState> hs(20);
-        launch_sample(t, sel, 0); launch_collect(t, sel, cand, 0); CK(hipDeviceSynchronize());
+        hipLaunchKernelGGL(k_sample_t<M_SAMPLE>, dim3(t.nseg), dim3(1024), 0, 0, t, sel);
+        hipLaunchKernelGGL((k_collect_t<2, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand);
+        CK(hipDeviceSynchronize());
         CK(hipMemcpy(hs.data(), sel, 20 * sizeof(SelState), hipMemcpyDeviceToHost));
-        for (int i = 0; i < 20; i += 3) { unsigned long long nc = 0, mxb = 0; for (int b = 0; b < NSUB_MAX; ++b) { nc += hs[i].sub[b]; mxb = std::max<unsigned long long>(mxb, hs[i].sub[b]); }
-            printf("  seg %2d n %8d below %8llu eql %llu eqh %llu cand %llu maxbucket %llu sh %u ovf %u\n", i, shapes[i], hs[i].below, hs[i].eq_lo, hs[i].eq_hi, nc, mxb, hs[i].shift, hs[i].overflow); }
-        launch_select(t, sel, cand, res, thr, 0); CK(hipDeviceSynchronize());
+        for (int i = 0; i < 20; i += 3) { unsigned long long bl = 0; for (int q = 0; q < NSHARD; ++q) bl += hs[i].below[q];
+            printf("  seg %2d n %8d below %8llu sh %u ovf %u kl %08x kh %08x\n", i, shapes[i], bl, hs[i].shift, hs[i].overflow, hs[i].kl, hs[i].kh); }
+        CK(hipMemset(sel, 0, selb)); CK(hipDeviceSynchronize());
+    }
+    {   // select phase timeline (100 MHz wall clock, per segment)
+        launch_sample(t, sel, 0); hipLaunchKernelGGL((k_collect_t<0, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand);
+        CK(hipDeviceSynchronize());
+        hipLaunchKernelGGL(k_select, dim3(t.nseg), dim3(SEL_THREADS), 0, 0, t, sel, cand, res, thr);
+        CK(hipDeviceSynchronize());
+        unsigned long long hp[24][8];
+        CK(hipMemcpyFromSymbol(hp, HIP_SYMBOL(g_probe), sizeof(hp)));
+        unsigned long long t0 = ~0ull; for (int i = 0; i < 20; ++i) t0 = std::min(t0, hp[i][0]);
+        for (int i = 0; i < 20; i += 3) { printf("  select seg %2d (us from first start):", i);
+            for (int k = 0; k < 7; ++k) printf(" %6.2f", hp[i][k] ? (double)(hp[i][k] - t0) / 100.0 : -1.0); printf("\n"); }
     }
     bench("empty-ish: k_synth 1 elem", [&]{ launch_synth(cx, 1, 0, 0, 30, 0); }, 0);
     // print result info

@@ -162,6 +162,8 @@ int plan_tensors(const wtp_tensor* ts, int n, int wid, int level, double pct, bo
                                                          : "shape is invalid for input of this size");
             }
         }
+        /* selection counts are kept in 32 bits on the device (8 GiB of float32 per tensor) */
+        if (p.pop > (int64_t)INT32_MAX) return fail(WTP_EARG, t, "tensor %d: more than 2^31-1 coefficients", t);
         p.cap = cap_for(p.pop);
     }
     return WTP_OK;
@@ -363,12 +365,10 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         if (first) stage(1, s);
         launch_sample(tab, sel, s);
         if (first) stage(2, s);
-        launch_collect(tab, sel, cand, s);
+        launch_collect_select(tab, sel, cand, results, thr_t, s);
         if (first) stage(3, s);
-        launch_select(tab, sel, cand, results, thr_t, s);
+        launch_mask(tab, thr_t, results, s);
         if (first) stage(4, s);
-        launch_mask(tab, thr_t, s);
-        if (first) stage(5, s);
     }
     /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2) */
     for (int t = 0; t < ntensors; ++t) {
@@ -378,7 +378,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         inverse(P, p, tp, thr_t + t, tensors[t].out,
                 reinterpret_cast<unsigned long long*>(&results[t].zero_count), tL, tH, tA, s);
     }
-    stage(6, s);
+    stage(5, s);
     return check_launch();
 }
 

@@ -6,12 +6,11 @@
  * bit pattern of |x| (a key monotone in |x|; NaN sorts last as in np.partition):
  *   k_sample   one block per segment: 32768 sampled keys histogrammed into 1/128-octave
  *              bins -> window [kl, kh] bracketing the order statistics r0, r0+1
- *   k_collect  stream once: count keys < kl, == kl, == kh, == 0; scatter the keys inside
- *              (kl, kh) into key-range buckets (one run per bucket per block); max key
- *   k_select   one block per segment: exact radix select of both ranks (from the one or two
- *              buckets that hold them, or the whole segment if the window missed), NumPy 1.x
- *              _lerp in f64, and the
- *              exact zero count of the level-0 output (from the window counts)
+ *   k_collect  stream once: count keys < kl, == kl, == kh; scatter the keys inside (kl, kh)
+ *              into key-range buckets (one run per bucket per block); max key
+ *   k_select   one block per segment: exact radix select of both ranks from the one or two
+ *              buckets that hold them (or the whole segment if the window missed), NumPy 1.x
+ *              _lerp in f64, and the exact zero count of the level-0 output from the counts
  *   k_mask     stream again: out = |x| < thr ? 0 : x                    (level-0 segments)
  * Filter bank (pywt.wavedec2 / waverec2 periodization, :67-77): separable one-level passes
  * whose every output is summed in PyWavelets' exact order (csrc/wt_dwt_core.h); the
@@ -35,27 +34,45 @@ __device__ __forceinline__ int find_seg(const SegTable& t, int b) {
     return s;
 }
 
+/* Cross-lane primitives on DPP (GFX9 wave64: row_shr inside rows of 16 lanes, row_bcast:15/31
+ * across rows): a few VALU cycles per step, where __shfl (ds_bpermute) pays an LDS round trip
+ * per step.  Every lane of the wave must be active. */
+template <int CTRL, int ROWM = 0xf, int BANKM = 0xf>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWM, BANKM, false);
+}
+
+/* inclusive prefix sum across the 64 lanes */
+__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t v) {
+    v += dpp_u32<0x111>(v); /* row_shr:1 */
+    v += dpp_u32<0x112>(v); /* row_shr:2 */
+    v += dpp_u32<0x114>(v); /* row_shr:4 */
+    v += dpp_u32<0x118>(v); /* row_shr:8 */
+    v += dpp_u32<0x142, 0xa>(v); /* row_bcast:15 into rows 1, 3 */
+    v += dpp_u32<0x143, 0xc>(v); /* row_bcast:31 into rows 2, 3 */
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_u32(v), 63);
+}
+
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
+    v = max(v, dpp_u32<0x111>(v));
+    v = max(v, dpp_u32<0x112>(v));
+    v = max(v, dpp_u32<0x114>(v));
+    v = max(v, dpp_u32<0x118>(v));
+    v = max(v, dpp_u32<0x142, 0xa>(v));
+    v = max(v, dpp_u32<0x143, 0xc>(v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+/* exact 64-bit sum (three 32-bit reductions of 16/16/32-bit fields) */
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-/* inclusive prefix sum across the 64 lanes of a wave */
-__device__ __forceinline__ int64_t wave_incl_scan(int64_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int64_t u = __shfl_up(v, o, 64);
-        if (lane >= o) v += u;
-    }
-    return v;
+    const uint32_t lo = wave_sum_u32((uint32_t)v & 0xFFFFu);
+    const uint32_t mid = wave_sum_u32((uint32_t)(v >> 16) & 0xFFFFu);
+    const uint32_t hi = wave_sum_u32((uint32_t)(v >> 32));
+    return ((unsigned long long)hi << 32) + ((unsigned long long)mid << 16) + lo;
 }
 
 /* block sum of an unsigned 64-bit value; result valid in thread 0 */
@@ -71,18 +88,20 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v
     return t;
 }
 
-/* 16 float4 per thread of one CHUNK (fully populated, 16-byte aligned) */
-__device__ __forceinline__ void load_chunk(const float* p, float4 (&v)[16]) {
+/* IT float4 per thread of one chunk (fully populated, 16-byte aligned) */
+template <int IT>
+__device__ __forceinline__ void load_chunk(const float* p, float4 (&v)[IT]) {
     const float4* p4 = reinterpret_cast<const float4*>(p);
 #pragma unroll
-    for (int it = 0; it < 16; ++it) v[it] = p4[it * STREAM_THREADS + threadIdx.x];
+    for (int it = 0; it < IT; ++it) v[it] = p4[it * STREAM_THREADS + threadIdx.x];
 }
 
 /* the float4 part of a ragged chunk (len4 float4s), all loads issued up front */
-__device__ __forceinline__ void load_chunk_part(const float* p, int len4, float4 (&v)[16]) {
+template <int IT>
+__device__ __forceinline__ void load_chunk_part(const float* p, int len4, float4 (&v)[IT]) {
     const float4* p4 = reinterpret_cast<const float4*>(p);
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int j = it * STREAM_THREADS + threadIdx.x;
         v[it] = j < len4 ? p4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -92,9 +111,9 @@ __device__ __forceinline__ void load_chunk_part(const float* p, int len4, float4
 /* Find the digit (8 bits) holding rank r in a 256-bin LDS histogram; one wave. */
 __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, int* digit, int64_t* below) {
     const int lane = threadIdx.x & 63;
-    const int64_t c0 = hb[4 * lane], c1 = hb[4 * lane + 1], c2 = hb[4 * lane + 2], c3 = hb[4 * lane + 3];
-    const int64_t s = c0 + c1 + c2 + c3;
-    const int64_t incl = wave_incl_scan(s);
+    const uint32_t c0 = hb[4 * lane], c1 = hb[4 * lane + 1], c2 = hb[4 * lane + 2], c3 = hb[4 * lane + 3];
+    const uint32_t s = c0 + c1 + c2 + c3; /* histograms count < 2^32 keys */
+    const int64_t incl = wave_scan_u32(s);
     int64_t cum = incl - s;
     if (r >= cum && r < incl) {
         int d = 4 * lane;
@@ -108,28 +127,34 @@ __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, i
 
 /* --------------------------------------------------------------- k_sample --- */
 constexpr int SAMPLE_THREADS = 1024;
-constexpr int SAMPLE_PER = M_SAMPLE / SAMPLE_THREADS; /* 32 */
 constexpr int FB_PER = (NB + SAMPLE_THREADS - 1) / SAMPLE_THREADS; /* 5 bins per thread */
 
-__global__ __launch_bounds__(SAMPLE_THREADS) void k_sample(SegTable t, SelState* __restrict__ sel) {
+template <int MS>
+__global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_t(SegTable t, SelState* __restrict__ sel) {
+    constexpr int SAMPLE_PER = MS / SAMPLE_THREADS;
     __shared__ uint32_t h[FB_PER * SAMPLE_THREADS];
     __shared__ int64_t wtot[SAMPLE_THREADS / 64];
     __shared__ int64_t found[4]; /* bin(sa), bin(sb) */
     const SegDesc& sd = t.s[blockIdx.x];
     const int64_t n = sd.n;
-    const bool exact = n <= M_SAMPLE;
-    const int m = exact ? (int)n : M_SAMPLE;
+    const bool exact = n <= MS;
+    const int m = exact ? (int)n : MS;
     const float* x = sd.data;
     /* sampled keys: groups of SAMPLE_GROUP contiguous floats spread evenly over the segment */
+    /* all loads unconditional and issued before any use (indices clamped; the sentinel marks
+     * the unused slots of a small segment) */
     uint32_t k[SAMPLE_PER];
-    const double step = exact ? 0.0 : (double)(n - SAMPLE_GROUP) / (double)(M_SAMPLE / SAMPLE_GROUP - 1);
+    const double step = exact ? 0.0 : (double)(n - SAMPLE_GROUP) / (double)(MS / SAMPLE_GROUP - 1);
 #pragma unroll
     for (int j = 0; j < SAMPLE_PER; ++j) {
         const int i = j * SAMPLE_THREADS + threadIdx.x;
-        int64_t pos = i;
-        if (!exact) pos = (int64_t)((double)(i / SAMPLE_GROUP) * step) + (i % SAMPLE_GROUP);
-        k[j] = (i < m) ? abs_key(x[pos]) : 0xFFFFFFFFu;
+        const int64_t pos = exact ? min((int64_t)i, n - 1)
+                                  : (int64_t)((double)(i / SAMPLE_GROUP) * step) + (i % SAMPLE_GROUP);
+        k[j] = abs_key(x[pos]);
     }
+#pragma unroll
+    for (int j = 0; j < SAMPLE_PER; ++j)
+        if (j * SAMPLE_THREADS + (int)threadIdx.x >= m) k[j] = 0xFFFFFFFFu;
     for (int i = threadIdx.x; i < FB_PER * SAMPLE_THREADS; i += SAMPLE_THREADS) h[i] = 0;
     if (threadIdx.x < 4) found[threadIdx.x] = -1;
     __syncthreads();
@@ -150,14 +175,14 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample(SegTable t, SelState*
         sa = (int64_t)floor(s0 - d);
         sb = (int64_t)ceil(s1 + d);
     }
-    int64_t local = 0;
+    uint32_t local = 0;
 #pragma unroll
     for (int j = 0; j < FB_PER; ++j) local += h[threadIdx.x * FB_PER + j];
-    const int64_t incl = wave_incl_scan(local);
+    const int64_t incl = wave_scan_u32(local);
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 63) wtot[wv] = incl;
     __syncthreads();
-    int64_t cum = incl - local;
+    int64_t cum = incl - (int64_t)local;
     for (int i = 0; i < wv; ++i) cum += wtot[i];
 #pragma unroll
     for (int j = 0; j < FB_PER; ++j) {
@@ -186,30 +211,31 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample(SegTable t, SelState*
     }
 }
 
-/* -------------------------------------------------------------- k_collect --- */
-constexpr int STAGE_CAP = 4096; /* inside keys staged per block before the bucket scatter */
+/* timing probes for tools/mb/lab.hip (empty in the library) */
+#ifndef WTP_PROBE
+#define WTP_PROBE(i)
+#endif
 
-__global__ __launch_bounds__(STREAM_THREADS) void k_collect(SegTable t, SelState* __restrict__ sel,
-                                                            uint32_t* __restrict__ cand) {
-    __shared__ uint32_t lsub[NSUB_MAX];  /* this block's keys per bucket, then the running offset */
-    __shared__ uint32_t lbase[NSUB_MAX]; /* reserved start of this block's run in each bucket     */
-    __shared__ uint32_t stage[STAGE_CAP];
-    __shared__ uint32_t wred[STREAM_THREADS / 64][5];
-    __shared__ int wtot[STREAM_THREADS / 64];
-    const int si = find_seg(t, blockIdx.x);
-    const SegDesc& sd = t.s[si];
-    const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * CHUNK;
-    const int len = (int)min((int64_t)CHUNK, sd.n - base);
+/* -------------------------------------------------------------- k_collect --- */
+/* LAB: 0 = the production kernel; 1 = stop after the counters; 2 = stop after staging
+ * (tools/mb/lab.hip ablations).  IT float4 per thread: a sub-chunk of IT * 1024 elements per
+ * block.  FULL: a whole 16-byte-aligned sub-chunk (unpredicated loads, so the compiler can
+ * count its waits); otherwise a ragged or unaligned one.  Up to a quarter of a sub-chunk's
+ * keys may fall inside the window (more: the select takes the full scan). */
+template <int IT, bool FULL, int LAB>
+__device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __restrict__ st,
+                                             uint32_t* __restrict__ cand, int64_t base, int len, uint32_t* lsub,
+                                             uint32_t* lbase, uint32_t* stage, uint32_t (*wred)[4], int* wtot) {
+    constexpr int SUB = IT * STREAM_THREADS * 4, STAGE_CAP = SUB / 4;
     const float* p = sd.data + base;
-    const bool vec = (sd.flags & SEG_ALIGNED) != 0;
-    const int len4 = vec ? len >> 2 : 0;
-    float4 v[16];
-    if (vec) load_chunk_part(p, len4, v); /* stream loads first: the window state arrives meanwhile */
-    SelState* st = sel + sd.slot;
+    const int len4 = FULL ? SUB / 4 : ((sd.flags & SEG_ALIGNED) ? len >> 2 : 0);
+    float4 v[IT];
+    if (FULL) load_chunk<IT>(p, v); /* stream loads first: the window state arrives meanwhile */
+    else load_chunk_part<IT>(p, len4, v);
     const uint32_t kl = st->kl, kh = st->kh, sh = st->shift;
     const int nsub = 1 << sd.nsub_log2;
     for (int i = threadIdx.x; i < nsub; i += STREAM_THREADS) lsub[i] = 0;
-    uint32_t below = 0, eql = 0, eqh = 0, zer = 0, mx = 0;
+    uint32_t below = 0, eql = 0, eqh = 0, mx = 0;
     int cnt = 0;
     auto inside = [&](uint32_t k) { return k > kl && k < kh; };
     auto tally = [&](float xv) {
@@ -218,30 +244,24 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_collect(SegTable t, SelState
         below += k < kl;
         eql += k == kl;
         eqh += (k == kh) & (kh != kl);
-        zer += k == 0;
         cnt += inside(k);
     };
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
-        if (it * STREAM_THREADS + (int)threadIdx.x < len4) {
+    for (int it = 0; it < IT; ++it) {
+        if (FULL || it * STREAM_THREADS + (int)threadIdx.x < len4) {
             tally(v[it].x); tally(v[it].y); tally(v[it].z); tally(v[it].w);
         }
     }
-    for (int i = len4 * 4 + threadIdx.x; i < len; i += STREAM_THREADS) tally(p[i]);
-    /* one block reduction for the five counters */
+    if (!FULL)
+        for (int i = len4 * 4 + threadIdx.x; i < len; i += STREAM_THREADS) tally(p[i]);
+    /* one block reduction for the counters */
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     {
-        uint32_t r[5] = {below, eql, eqh, zer, mx};
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) r[q] += (uint32_t)__shfl_xor((int)r[q], o, 64);
-            r[4] = max(r[4], (uint32_t)__shfl_xor((int)r[4], o, 64));
-        }
-        if (lane == 0)
-            for (int q = 0; q < 5; ++q) wred[wv][q] = r[q];
+        const uint32_t r0 = wave_sum_u32(below), r1 = wave_sum_u32(eql), r2 = wave_sum_u32(eqh),
+                       r3 = wave_max_u32(mx);
+        if (lane == 0) { wred[wv][0] = r0; wred[wv][1] = r1; wred[wv][2] = r2; wred[wv][3] = r3; }
     }
-    const int incl = (int)wave_incl_scan(cnt);
+    const int incl = (int)wave_scan_u32((uint32_t)cnt);
     if (lane == 63) wtot[wv] = incl;
     __syncthreads();
     int off = incl - cnt, total = 0;
@@ -250,38 +270,41 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_collect(SegTable t, SelState
         total += wtot[i];
     }
     if (threadIdx.x == 0) {
-        unsigned long long a[4] = {0, 0, 0, 0};
+        unsigned long long a[3] = {0, 0, 0};
         uint32_t m2 = 0;
         for (int w = 0; w < STREAM_THREADS / 64; ++w) {
-            for (int q = 0; q < 4; ++q) a[q] += wred[w][q];
-            m2 = max(m2, wred[w][4]);
+            for (int q = 0; q < 3; ++q) a[q] += wred[w][q];
+            m2 = max(m2, wred[w][3]);
         }
-        if (a[0]) atomicAdd(&st->below, a[0]);
-        if (a[1]) atomicAdd(&st->eq_lo, a[1]);
-        if (a[2]) atomicAdd(&st->eq_hi, a[2]);
-        if (a[3]) atomicAdd(&st->zeros, a[3]);
-        atomicMax(&st->maxkey, m2);
+        const int sh8 = blockIdx.x & (NSHARD - 1);
+        if (a[0]) atomicAdd(&st->below[sh8], a[0]);
+        if (a[1]) atomicAdd(&st->eq_lo[sh8], a[1]);
+        if (a[2]) atomicAdd(&st->eq_hi[sh8], a[2]);
+        atomicMax(&st->maxkey[sh8], m2);
         if (total > STAGE_CAP) atomicOr(&st->overflow, 1u);
     }
-    if (total == 0 || total > STAGE_CAP) return; /* uniform; an overflow sends k_select to the full scan */
+    /* uniform: nothing inside the window here, or too much (the select then takes the full scan) */
+    if (LAB == 1 || total == 0 || total > STAGE_CAP) return;
     /* stage this block's inside keys, count them per bucket */
     if (cnt) {
         int pos = off;
 #pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            if (it * STREAM_THREADS + (int)threadIdx.x < len4) {
+        for (int it = 0; it < IT; ++it) {
+            if (FULL || it * STREAM_THREADS + (int)threadIdx.x < len4) {
                 const uint32_t k4[4] = {abs_key(v[it].x), abs_key(v[it].y), abs_key(v[it].z), abs_key(v[it].w)};
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
                     if (inside(k4[c])) stage[pos++] = k4[c];
             }
         }
-        for (int i = len4 * 4 + threadIdx.x; i < len; i += STREAM_THREADS) {
-            const uint32_t k = abs_key(p[i]);
-            if (inside(k)) stage[pos++] = k;
-        }
+        if (!FULL)
+            for (int i = len4 * 4 + threadIdx.x; i < len; i += STREAM_THREADS) {
+                const uint32_t k = abs_key(p[i]);
+                if (inside(k)) stage[pos++] = k;
+            }
     }
     __syncthreads();
+    if (LAB == 2) return;
     for (int i = threadIdx.x; i < total; i += STREAM_THREADS) atomicAdd(&lsub[(stage[i] - kl - 1) >> sh], 1u);
     __syncthreads();
     /* reserve one contiguous run per non-empty bucket (one returning atomic per bucket) */
@@ -297,14 +320,11 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_collect(SegTable t, SelState
         const uint32_t k = stage[i];
         const uint32_t b = (k - kl - 1) >> sh;
         const uint32_t at = lbase[b] + atomicAdd(&lsub[b], 1u);
-        if (at < bcap) out[(int64_t)b * bcap + at] = k; /* counted beyond capacity: k_select sees it */
+        if (at < bcap) out[(int64_t)b * bcap + at] = k; /* counted beyond capacity: the select sees it */
     }
 }
 
-/* --------------------------------------------------------------- k_select --- */
-constexpr int SEL_THREADS = 1024;
-constexpr int SEL_STAGE = 16384; /* filtered candidates staged in LDS */
-
+/* ------------------------------------------------------------- the select --- */
 /* Radix select of ranks ra / rb among keys that all lie in [lo, hi]: the bits above the
  * highest bit where lo and hi differ are common and skipped (concentrated digits are what
  * makes an MSB-first LDS histogram contend). */
@@ -352,32 +372,23 @@ __device__ int64_t block_count_below(const Get& get, int64_t m, uint32_t tk) {
     __shared__ unsigned long long acc;
     if (threadIdx.x == 0) acc = 0;
     __syncthreads();
-    unsigned long long c = 0;
+    uint32_t c = 0; /* per thread < 2^32 */
     for (int64_t i = threadIdx.x; i < m; i += THREADS) c += get(i) < tk;
-    c = wave_sum_u64(c);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&acc, c);
+    const unsigned long long w = wave_sum_u64(c);
+    if ((threadIdx.x & 63) == 0 && w) atomicAdd(&acc, w);
     __syncthreads();
     const int64_t r = (int64_t)acc;
     __syncthreads();
     return r;
 }
 
-/* inclusive prefix over nsub bucket counts held in global memory; one wave.  Returns the
- * total and, for rank r (if found), its bucket and the count before it. */
-__device__ __forceinline__ int64_t wave_bucket_total(const uint32_t* sub, int nsub) {
-    const int lane = threadIdx.x & 63;
-    unsigned long long s = 0;
-    for (int b = lane; b < nsub; b += 64) s += sub[b];
-    return (int64_t)wave_sum_u64(s);
-}
-
 __device__ __forceinline__ void wave_find_bucket(const uint32_t* sub, int nsub, int64_t r, int* bucket,
                                                  int64_t* before) {
     const int lane = threadIdx.x & 63;
     const int per = nsub / 64; /* 1..16 consecutive buckets per lane */
-    int64_t s = 0;
+    uint32_t s = 0; /* bucket counts of one segment: < 2^32 */
     for (int j = 0; j < per; ++j) s += sub[lane * per + j];
-    const int64_t incl = wave_incl_scan(s);
+    const int64_t incl = wave_scan_u32(s);
     int64_t cum = incl - s;
     if (r >= cum && r < incl) {
         for (int j = 0; j < per; ++j) {
@@ -388,25 +399,51 @@ __device__ __forceinline__ void wave_find_bucket(const uint32_t* sub, int nsub, 
     }
 }
 
-__global__ __launch_bounds__(SEL_THREADS) void k_select(SegTable t, SelState* __restrict__ sel,
-                                                        const uint32_t* __restrict__ cand,
-                                                        wtp_result* __restrict__ res, float* __restrict__ thr_out) {
-    __shared__ uint32_t stage[SEL_STAGE];
+/* Resolve the two order statistics of one segment from its counters and buckets, compute the
+ * NumPy threshold and the level-0 zero count, publish the results, and leave the slot clean.
+ * One block of THREADS threads; `stage` holds up to stage_cap keys in LDS. */
+template <int THREADS>
+__device__ void select_body(const SegDesc& sd, SelState* __restrict__ st, const uint32_t* __restrict__ cand,
+                            wtp_result* __restrict__ res, float* __restrict__ thr_out, uint32_t* stage,
+                            int stage_cap) {
     __shared__ int sbin[2];
     __shared__ int64_t sbefore[2];
-    __shared__ int64_t s_ncand;
-    const SegDesc& sd = t.s[blockIdx.x];
-    SelState* st = sel + sd.slot;
+    __shared__ uint32_t lsub[NSUB_MAX];
+    __shared__ unsigned long long s_cnt[4]; /* below, eq_lo, eq_hi, inside */
+    __shared__ uint32_t s_mk, s_ovf;
     const int nsub = 1 << sd.nsub_log2;
     const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
-    const int64_t below = (int64_t)st->below, eql = (int64_t)st->eq_lo, eqh = (int64_t)st->eq_hi;
     const uint32_t kl = st->kl, kh = st->kh, sh = st->shift;
+    WTP_PROBE(0);
+    /* one round trip: threads 0..4 gather the sharded counters, wave 1 the bucket counts (to LDS) */
     if (threadIdx.x < 64) {
-        const int64_t tot = wave_bucket_total(st->sub, nsub);
-        if (threadIdx.x == 0) s_ncand = tot;
+        const int l = threadIdx.x;
+        if (l < 3) {
+            const unsigned long long* a = l == 0 ? st->below : (l == 1 ? st->eq_lo : st->eq_hi);
+            unsigned long long v = 0;
+#pragma unroll
+            for (int i = 0; i < NSHARD; ++i) v += a[i];
+            s_cnt[l] = v;
+        } else if (l == 3) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int i = 0; i < NSHARD; ++i) m = max(m, st->maxkey[i]);
+            s_mk = m;
+        } else if (l == 4) {
+            s_ovf = st->overflow;
+        }
+    } else if (threadIdx.x < 128) {
+        const int l = threadIdx.x - 64;
+        uint32_t sm = 0;
+        for (int b = l; b < nsub; b += 64) { const uint32_t v = st->sub[b]; lsub[b] = v; sm += v; }
+        sm = wave_sum_u32(sm);
+        if (l == 0) s_cnt[3] = sm;
     }
     __syncthreads();
-    const int64_t ncand = s_ncand;
+    WTP_PROBE(1);
+    const int64_t below = (int64_t)s_cnt[0], eql = (int64_t)s_cnt[1], eqh = (int64_t)s_cnt[2];
+    const int64_t ncand = (int64_t)s_cnt[3];
+    uint32_t mk = s_mk;
     /* class of a rank: 0 miss, 1 == kl, 2 inside, 3 == kh */
     auto classify = [&](int64_t r, int64_t* j) {
         if (r < below) return 0;
@@ -422,39 +459,46 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(SegTable t, SelState* __
     const int ca = classify(r0, &ja), cb = classify(r1, &jb);
     const float* x = sd.data;
     const int64_t bcap = sd.bucket_cap;
+    const uint32_t* c = cand + sd.cand_off;
     uint32_t ka = 0, kb = 0;
     int path = MODE_WINDOW;
-    int nst = 0;           /* staged keys (the buckets holding inside ranks) */
-    int64_t before = 0;    /* inside keys in the buckets below the staged ones */
-    bool full = ca == 0 || cb == 0 || st->overflow != 0;
+    int64_t nlo = 0, nhi = 0, before = 0;
+    int blo = 0, bhi = 0;
+    bool in_lds = false;
+    bool full = ca == 0 || cb == 0 || s_ovf != 0;
     if (!full && (ca == 2 || cb == 2)) {
-        if (threadIdx.x < 64) {
-            if (ca == 2) wave_find_bucket(st->sub, nsub, ja, &sbin[0], &sbefore[0]);
-            if (cb == 2) wave_find_bucket(st->sub, nsub, jb, &sbin[1], &sbefore[1]);
-        }
+        if (threadIdx.x < 64 && ca == 2) wave_find_bucket(lsub, nsub, ja, &sbin[0], &sbefore[0]);
+        if (threadIdx.x >= 64 && threadIdx.x < 128 && cb == 2) wave_find_bucket(lsub, nsub, jb, &sbin[1], &sbefore[1]);
         __syncthreads();
-        const int blo = (ca == 2) ? sbin[0] : sbin[1];
-        const int bhi = (cb == 2) ? sbin[1] : sbin[0];
+        WTP_PROBE(2);
+        blo = (ca == 2) ? sbin[0] : sbin[1];
+        bhi = (cb == 2) ? sbin[1] : sbin[0];
         before = (ca == 2) ? sbefore[0] : sbefore[1];
         /* adjacent ranks: buckets strictly between blo and bhi are empty */
-        const int64_t nlo = st->sub[blo], nhi = (bhi != blo) ? st->sub[bhi] : 0;
+        nlo = lsub[blo];
+        nhi = (bhi != blo) ? lsub[bhi] : 0;
         if (nlo > bcap || nhi > bcap) {
             full = true;
         } else {
-            const uint32_t* c = cand + sd.cand_off;
-            for (int i = threadIdx.x; i < nlo; i += SEL_THREADS) stage[i] = c[(int64_t)blo * bcap + i];
-            for (int i = threadIdx.x; i < nhi; i += SEL_THREADS) stage[nlo + i] = c[(int64_t)bhi * bcap + i];
-            nst = (int)(nlo + nhi);
-            __syncthreads();
+            in_lds = nlo + nhi <= stage_cap;
+            if (in_lds) {
+                for (int i = threadIdx.x; i < nlo; i += THREADS) stage[i] = c[(int64_t)blo * bcap + i];
+                for (int i = threadIdx.x; i < nhi; i += THREADS) stage[nlo + i] = c[(int64_t)bhi * bcap + i];
+                __syncthreads();
+            }
+            WTP_PROBE(3);
             const uint64_t lo64 = (uint64_t)kl + 1 + ((uint64_t)blo << sh);
             const uint64_t hi64 = min((uint64_t)kh - 1, (uint64_t)kl + ((uint64_t)(bhi + 1) << sh));
             uint32_t xa = 0, xb = 0;
-            select_in_range<SEL_THREADS>([&](int64_t i) { return stage[i]; }, [](uint32_t) { return true; },
-                                         (int64_t)nst, (uint32_t)lo64, (uint32_t)hi64, ja - before, jb - before,
-                                         ca == 2, cb == 2, &xa, &xb);
+            auto getb = [&](int64_t i) {
+                return in_lds ? stage[i] : (i < nlo ? c[(int64_t)blo * bcap + i] : c[(int64_t)bhi * bcap + i - nlo]);
+            };
+            select_in_range<THREADS>(getb, [](uint32_t) { return true; }, nlo + nhi, (uint32_t)lo64,
+                                     (uint32_t)hi64, ja - before, jb - before, ca == 2, cb == 2, &xa, &xb);
             ka = (ca == 2) ? xa : (ca == 1 ? kl : kh);
             kb = (cb == 2) ? xb : (cb == 1 ? kl : kh);
             path = MODE_CAND;
+            WTP_PROBE(4);
         }
     } else if (!full) {
         ka = (ca == 1) ? kl : kh;
@@ -462,34 +506,39 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(SegTable t, SelState* __
     }
     if (full) {
         /* the window missed (or a block/bucket overflowed): exact radix select over the segment */
-        select_in_range<SEL_THREADS>([&](int64_t i) { return abs_key(x[i]); }, [](uint32_t) { return true; }, sd.n, 0u,
-                                     0xFFFFFFFFu, r0, r1, true, true, &ka, &kb);
+        select_in_range<THREADS>([&](int64_t i) { return abs_key(x[i]); }, [](uint32_t) { return true; }, sd.n, 0u,
+                                 0xFFFFFFFFu, r0, r1, true, true, &ka, &kb);
         path = MODE_FULL;
     }
     __syncthreads();
     /* threshold: numpy/lib/function_base.py _lerp -- diff in float32, the blend in float64 */
-    const uint32_t mk = st->maxkey;
     const float fa = __uint_as_float(ka), fb = __uint_as_float(kb);
     const float diff = fb - fa;
     const double g = sd.gamma;
     double thr = (g >= 0.5) ? (double)fb - (double)diff * (1.0 - g) : (double)fa + (double)diff * g;
-    if (mk > 0x7F800000u) thr = __longlong_as_double(0x7FF8000000000000ll); /* NaN present */
+    if (mk > 0x7F800000u) thr = __longlong_as_double(0x7FF8000000000000ll); /* NaN present: np.percentile is NaN */
     const float thr32 = (float)thr;
-    /* level-0 segments: zeros of where(|x| < thr, 0, x) = #(|x| < thr) + [not (0 < thr)] * #(x == 0).
-     * ka <= thr <= kb, so #(key < thr) = below + [thr > kl] eq_lo + before + #(staged < thr). */
+    const bool nan = thr32 != thr32; /* also inf - inf inside the lerp */
+    /* level-0 segments: zeros of where(|x| < thr, 0, x) = #(key < tk) with tk = bits(thr) when
+     * thr > 0, else tk = 1 (only the zeros themselves).  ka <= thr <= kb and the two ranks are
+     * adjacent, so #(key < tk) = below + [tk > kl] eq_lo + before + #(staged < tk).  A NaN
+     * threshold prunes nothing: k_mask counts the zeros of the copy. */
+    WTP_PROBE(5);
     int64_t zc = 0;
-    if (sd.flags & SEG_MASK) {
-        if (thr32 > 0.0f) {
-            const uint32_t tk = __float_as_uint(thr32);
-            if (path == MODE_FULL)
-                zc = block_count_below<SEL_THREADS>([&](int64_t i) { return abs_key(x[i]); }, sd.n, tk);
-            else
-                zc = below + (tk > kl ? eql : 0) + before +
-                     block_count_below<SEL_THREADS>([&](int64_t i) { return stage[i]; }, nst, tk) +
-                     (tk > kh ? eqh : 0);
-        } else {
-            zc = (int64_t)st->zeros;
-        }
+    if ((sd.flags & SEG_MASK) && !nan) {
+        const uint32_t tk = thr32 > 0.0f ? __float_as_uint(thr32) : 1u;
+        if (path == MODE_FULL)
+            zc = block_count_below<THREADS>([&](int64_t i) { return abs_key(x[i]); }, sd.n, tk);
+        else if (path == MODE_CAND)
+            zc = below + (tk > kl ? eql : 0) + before +
+                 block_count_below<THREADS>(
+                     [&](int64_t i) {
+                         return in_lds ? stage[i]
+                                       : (i < nlo ? c[(int64_t)blo * bcap + i] : c[(int64_t)bhi * bcap + i - nlo]);
+                     },
+                     nlo + nhi, tk);
+        else
+            zc = below + (tk > kl ? eql : 0);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -498,53 +547,110 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(SegTable t, SelState* __
         st->key_a = ka;
         st->key_b = kb;
         st->mode = path;
-        /* leave the slot clean for the next call */
-        st->overflow = 0;
-        st->maxkey = 0;
-        st->below = 0;
-        st->eq_lo = 0;
-        st->eq_hi = 0;
-        st->zeros = 0;
+        st->overflow = 0; /* leave the slot clean for the next call */
         wtp_result& r = res[sd.res];
         r.numel = sd.numel;
         r.coeff_numel = sd.n;
-        r.zero_count = zc; /* DWT segments: the inverse transform adds the zeros of its output */
+        r.zero_count = zc; /* DWT segments / NaN thresholds: a later kernel adds the zeros it writes */
         r.thr64 = thr;
         r.thr32_bits = __float_as_uint(thr32);
         r.max_abs_bits = mk;
         r.eff_level = sd.eff_level;
         r.path = path;
     }
-    for (int i = threadIdx.x; i < nsub; i += SEL_THREADS) st->sub[i] = 0;
+    WTP_PROBE(6);
+    for (int i = threadIdx.x; i < nsub; i += THREADS) st->sub[i] = 0;
+    if (threadIdx.x < NSHARD) {
+        st->below[threadIdx.x] = 0;
+        st->eq_lo[threadIdx.x] = 0;
+        st->eq_hi[threadIdx.x] = 0;
+        st->maxkey[threadIdx.x] = 0;
+    }
+}
+
+/* one block per sub-chunk: block b takes sub-chunk (b % SPLIT) of table block (b / SPLIT) */
+template <int LAB, int IT>
+__global__ __launch_bounds__(STREAM_THREADS) void k_collect_t(SegTable t, SelState* __restrict__ sel,
+                                                              uint32_t* __restrict__ cand) {
+    constexpr int SUB = IT * STREAM_THREADS * 4, SPLIT = CHUNK / SUB;
+    static_assert(CHUNK % SUB == 0, "sub-chunk size");
+    __shared__ uint32_t lsub[NSUB_MAX];  /* this block's keys per bucket, then the running offset */
+    __shared__ uint32_t lbase[NSUB_MAX]; /* reserved start of this block's run in each bucket     */
+    __shared__ uint32_t stage[SUB / 4];
+    __shared__ uint32_t wred[STREAM_THREADS / 64][4];
+    __shared__ int wtot[STREAM_THREADS / 64];
+    const int tb = blockIdx.x / SPLIT;
+    const int si = find_seg(t, tb);
+    const SegDesc& sd = t.s[si];
+    const int64_t base = (int64_t)(tb - sd.blk_begin) * CHUNK + (int64_t)(blockIdx.x % SPLIT) * SUB;
+    const int len = (int)max((int64_t)0, min((int64_t)SUB, sd.n - base));
+    if (len == 0) return; /* past the end of the segment's last chunk */
+    SelState* st = sel + sd.slot;
+    if ((sd.flags & SEG_ALIGNED) && len == SUB)
+        collect_body<IT, true, LAB>(sd, st, cand, base, len, lsub, lbase, stage, wred, wtot);
+    else
+        collect_body<IT, false, LAB>(sd, st, cand, base, len, lsub, lbase, stage, wred, wtot);
+}
+
+/* k_select: one 1024-thread block per segment (separate launch: the kernel boundary is the
+ * inter-workgroup publish of k_collect's buckets; an in-kernel last-block ticket costs an
+ * agent-scope L2 write-back per block, measured slower on MI355X). */
+constexpr int SEL_THREADS = 1024, SEL_STAGE = 16384;
+__global__ __launch_bounds__(SEL_THREADS) void k_select(SegTable t, SelState* __restrict__ sel,
+                                                        const uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
+                                                        float* __restrict__ thr_out) {
+    __shared__ uint32_t stage[SEL_STAGE];
+    const SegDesc& sd = t.s[blockIdx.x];
+    select_body<SEL_THREADS>(sd, sel + sd.slot, cand, res, thr_out, stage, SEL_STAGE);
 }
 
 /* ----------------------------------------------------------------- k_mask --- */
 /* out = where(|x| < thr, 0, x) for level-0 segments; the zero count came from k_select. */
-__global__ __launch_bounds__(STREAM_THREADS) void k_mask(SegTable t, const float* __restrict__ thr_t) {
-    const int si = find_seg(t, blockIdx.x);
-    const SegDesc& sd = t.s[si];
-    if (!(sd.flags & SEG_MASK)) return;
-    const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * CHUNK;
-    const int len = (int)min((int64_t)CHUNK, sd.n - base);
+template <bool FULL>
+__device__ __forceinline__ unsigned long long mask_body(const SegDesc& sd, int64_t base, int len, float thr) {
     const float* p = sd.data + base;
     float* q = sd.out + base;
-    const bool vec = (sd.flags & SEG_ALIGNED) != 0;
-    const int len4 = vec ? len >> 2 : 0;
+    const int len4 = FULL ? CHUNK / 4 : ((sd.flags & SEG_ALIGNED) ? len >> 2 : 0);
     float4 v[16];
-    if (vec) load_chunk_part(p, len4, v);
-    const float thr = thr_t[sd.res];
-    auto f = [&](float xv) { return (fabsf(xv) < thr) ? 0.0f : xv; };
+    if (FULL) load_chunk<16>(p, v);
+    else load_chunk_part<16>(p, len4, v);
+    unsigned long long z = 0;
+    auto f = [&](float xv) {
+        const float y = (fabsf(xv) < thr) ? 0.0f : xv;
+        z += y == 0.0f;
+        return y;
+    };
     float4* q4 = reinterpret_cast<float4*>(q);
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
         const int j = it * STREAM_THREADS + threadIdx.x;
-        if (j < len4) {
+        if (FULL || j < len4) {
             float4 y;
             y.x = f(v[it].x); y.y = f(v[it].y); y.z = f(v[it].z); y.w = f(v[it].w);
             q4[j] = y;
         }
     }
-    for (int i = len4 * 4 + threadIdx.x; i < len; i += STREAM_THREADS) q[i] = f(p[i]);
+    if (!FULL)
+        for (int i = len4 * 4 + threadIdx.x; i < len; i += STREAM_THREADS) q[i] = f(p[i]);
+    return z;
+}
+
+/* out = where(|x| < thr, 0, x) for level-0 segments; the zero count came from the select,
+ * except for a NaN threshold (nothing pruned), where the zeros of the copy are counted here. */
+__global__ __launch_bounds__(STREAM_THREADS) void k_mask(SegTable t, const float* __restrict__ thr_t,
+                                                         wtp_result* __restrict__ res) {
+    const int si = find_seg(t, blockIdx.x);
+    const SegDesc& sd = t.s[si];
+    if (!(sd.flags & SEG_MASK)) return;
+    const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * CHUNK;
+    const int len = (int)min((int64_t)CHUNK, sd.n - base);
+    const float thr = thr_t[sd.res];
+    const unsigned long long z = ((sd.flags & SEG_ALIGNED) && len == CHUNK) ? mask_body<true>(sd, base, len, thr)
+                                                                            : mask_body<false>(sd, base, len, thr);
+    if (thr != thr) { /* uniform */
+        const unsigned long long tot = block_sum_u64<STREAM_THREADS>(z);
+        if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long*)&res[sd.res].zero_count, tot);
+    }
 }
 
 /* ------------------------------------------------------------ filter bank --- */
@@ -680,17 +786,16 @@ static inline unsigned grid_for(int64_t total) {
 }
 
 void launch_sample(const SegTable& t, SelState* sel, hipStream_t s) {
-    hipLaunchKernelGGL(k_sample, dim3(t.nseg), dim3(SAMPLE_THREADS), 0, s, t, sel);
+    hipLaunchKernelGGL(k_sample_t<M_SAMPLE>, dim3(t.nseg), dim3(SAMPLE_THREADS), 0, s, t, sel);
 }
-void launch_collect(const SegTable& t, SelState* sel, uint32_t* cand, hipStream_t s) {
-    hipLaunchKernelGGL(k_collect, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, sel, cand);
-}
-void launch_select(const SegTable& t, SelState* sel, const uint32_t* cand, wtp_result* res, float* thr_out,
-                   hipStream_t s) {
+void launch_collect_select(const SegTable& t, SelState* sel, uint32_t* cand, wtp_result* res, float* thr_out,
+                           hipStream_t s) {
+    hipLaunchKernelGGL((k_collect_t<0, COLLECT_IT>), dim3(t.nblk * (CHUNK / (COLLECT_IT * STREAM_THREADS * 4))),
+                       dim3(STREAM_THREADS), 0, s, t, sel, cand);
     hipLaunchKernelGGL(k_select, dim3(t.nseg), dim3(SEL_THREADS), 0, s, t, sel, cand, res, thr_out);
 }
-void launch_mask(const SegTable& t, const float* thr, hipStream_t s) {
-    hipLaunchKernelGGL(k_mask, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, thr);
+void launch_mask(const SegTable& t, const float* thr, wtp_result* res, hipStream_t s) {
+    hipLaunchKernelGGL(k_mask, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, thr, res);
 }
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
                      hipStream_t s) {

@@ -20,7 +20,7 @@ namespace wtp {
  * < kl, == kl, == kh and == 0 and scattering the keys strictly inside (kl, kh) into nsub
  * key-range buckets; k_select reads only the bucket(s) holding the two ranks and resolves
  * them exactly, or by a full radix select over the segment if the window missed. */
-constexpr int M_SAMPLE = 32768;
+constexpr int M_SAMPLE = 8192;
 constexpr int SAMPLE_GROUP = 16;   /* contiguous keys per sample group */
 constexpr int NSUB_MAX = 1024;     /* buckets over (kl, kh): 64..1024 per segment (SegDesc) */
 constexpr int BUCKET_MAX = 8192;   /* keys per bucket (two buckets are staged in LDS)       */
@@ -50,6 +50,7 @@ __host__ __device__ __forceinline__ uint32_t bin_hi_key(int b) { /* exclusive; 0
 
 /* ---- grouped launches over segments (one segment = one selection population) ---- */
 constexpr int CHUNK = 16384;        /* elements per block in the streaming passes */
+constexpr int COLLECT_IT = 16;      /* float4 per thread in k_collect (sub-chunks of CHUNK) */
 constexpr int STREAM_THREADS = 256; /* 64 elements = 16 float4 per thread          */
 constexpr int SEG_PER_LAUNCH = 24;
 
@@ -89,22 +90,26 @@ struct SegTable {
  * (0..SEG_PER_LAUNCH-1); the SelState slots sit at the very start of every workspace
  * layout, so every call sees the same persistent region: zeroed once by wtp_workspace_init
  * and left zeroed (counters) by every call -- k_select clears what k_collect accumulated. */
-struct SelState {
-    uint32_t maxkey;             /* atomicMax (k_collect)                                 */
-    uint32_t overflow;           /* a block had more inside keys than it can stage        */
-    unsigned long long below;    /* atomicAdd (k_collect): keys < kl                       */
-    unsigned long long eq_lo;    /* keys == kl                                            */
-    unsigned long long eq_hi;    /* keys == kh (kh != kl)                                 */
-    unsigned long long zeros;    /* keys == 0                                             */
-    uint32_t kl, kh;             /* window (k_sample); kh = 0xFFFFFFFF: unbounded          */
-    uint32_t shift;              /* bucket of an inside key = (key - kl - 1) >> shift      */
-    int32_t mode;                /* MODE_* chosen by k_select (diagnostics)                */
-    float thr32;                 /* the float32 threshold the compare uses                 */
-    uint32_t key_a, key_b;       /* resolved order statistics                              */
-    uint32_t pad[15];
-    uint32_t sub[NSUB_MAX];      /* keys per bucket (returning atomicAdd, k_collect)       */
+constexpr int NSHARD = 8; /* k_collect's per-segment counters are sharded by block (contention) */
+/* Field groups sit on separate 128-byte lines: counters (atomics), window parameters (read by
+ * every k_collect block), bucket counts. */
+struct alignas(128) SelState {
+    unsigned long long below[NSHARD]; /* atomicAdd (k_collect): keys < kl                    */
+    unsigned long long eq_lo[NSHARD]; /* keys == kl                                          */
+    unsigned long long eq_hi[NSHARD]; /* keys == kh (kh != kl)                               */
+    unsigned long long spare[NSHARD];
+    uint32_t maxkey[NSHARD];          /* atomicMax (k_collect)                               */
+    uint32_t overflow;                /* a block had more inside keys than it can stage     */
+    uint32_t pad0[23];
+    uint32_t kl, kh;                  /* window (k_sample); kh = 0xFFFFFFFF: unbounded       */
+    uint32_t shift;                   /* bucket of an inside key = (key - kl - 1) >> shift   */
+    int32_t mode;                     /* MODE_* chosen by the select (diagnostics)           */
+    float thr32;                      /* the float32 threshold the compare uses              */
+    uint32_t key_a, key_b;            /* resolved order statistics                           */
+    uint32_t pad1[25];
+    uint32_t sub[NSUB_MAX];           /* keys per bucket (returning atomicAdd, k_collect)    */
 };
-static_assert(sizeof(SelState) % 64 == 0, "SelState padding");
+static_assert(sizeof(SelState) % 128 == 0 && sizeof(SelState) == 4608, "SelState layout");
 
 enum SelMode : int32_t { MODE_CAND = 1, MODE_WINDOW = 2, MODE_FULL = 3 };
 
@@ -117,10 +122,9 @@ struct Taps {
 
 /* ---- launchers (kernels.hip) ---- */
 void launch_sample(const SegTable& t, SelState* sel, hipStream_t s);
-void launch_collect(const SegTable& t, SelState* sel, uint32_t* cand, hipStream_t s);
-void launch_select(const SegTable& t, SelState* sel, const uint32_t* cand, wtp_result* res, float* thr_out,
-                   hipStream_t s);
-void launch_mask(const SegTable& t, const float* thr, hipStream_t s);
+void launch_collect_select(const SegTable& t, SelState* sel, uint32_t* cand, wtp_result* res, float* thr_out,
+                           hipStream_t s);
+void launch_mask(const SegTable& t, const float* thr, wtp_result* res, hipStream_t s);
 
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
                      hipStream_t s);
