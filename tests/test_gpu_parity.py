@@ -140,6 +140,25 @@ def test_window_paths_and_extremes(eng):
         assert G.f64_bits_equal(r["thr64"], rr["thr64"]), pct
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 7, 4097, 16383, 16385, 2 * 16384 + 4099, 100_003])
+def test_ragged_and_unaligned_level0(eng, n):
+    """Level-0 populations of every length class (n % 4, partial last chunk), from 16-byte
+    aligned and unaligned (offset by one float) device pointers, in one batched call."""
+    rng = np.random.default_rng(n)
+    x = (rng.standard_normal(n + 1) * 0.05).astype(np.float32)
+    x[rng.integers(0, n, max(1, n // 50))] = 0.0
+    base = _dev(x)
+    aligned, unaligned = base[:n].clone(), base[1:n + 1]
+    assert unaligned.data_ptr() % 16 != 0
+    out_u = torch.empty(n + 1, dtype=torch.float32, device=base.device)[1:]
+    outs, res = eng.prune([aligned, unaligned], "db8", 5, 38.2, outs=[torch.empty_like(aligned), out_u],
+                          carry_level=False)
+    for xin, o, r in zip((x[:n], x[1:n + 1]), outs, res):
+        ref, rr = O.prune_tensor(xin.copy(), "db8", 5, 38.2)
+        assert np.array_equal(o.cpu().numpy(), ref)
+        assert r["zero_count"] == rr["zero_count"] and G.f64_bits_equal(r["thr64"], rr["thr64"])
+
+
 def test_in_place_and_workspace_reuse(eng):
     ts = G.W.resnet18_tensors(0)[:6]
     xs = [eng.synth(s, seed, tid, e) for _, s, seed, tid, e in ts]

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 __device__ unsigned long long g_probe[24][8];
 #define WTP_PROBE(i) do { if (threadIdx.x == 0) g_probe[blockIdx.x][i] = wall_clock64(); } while (0)
+__device__ unsigned long long g_cprobe[1024][8];
+#define WTP_CPROBE(i) do { if (threadIdx.x == 0 && blockIdx.x < 1024 && blockDim.x == 256) g_cprobe[blockIdx.x][i] = wall_clock64(); } while (0)
 #include "../../wavelettransforms_amd/csrc/kernels.hip"
 #include <cstdio>
 #include <cstring>
@@ -18,6 +20,12 @@ __global__ void k_dpp_test(const uint32_t* in, uint32_t* scan, uint32_t* mx, uns
     scan[blockIdx.x * 256 + threadIdx.x] = wave_scan_u32(v);
     mx[blockIdx.x * 256 + threadIdx.x] = wave_max_u32(v);
     sum64[blockIdx.x * 256 + threadIdx.x] = wave_sum_u64(((unsigned long long)v << 20) ^ v);
+}
+
+__global__ void k_ragged_test(const float* p, int len, float* out) {
+    float4 v[16];
+    load_chunk_ragged<16>(p, len, v);
+    for (int it = 0; it < 16; ++it) reinterpret_cast<float4*>(out)[it * 256 + threadIdx.x] = v[it];
 }
 
 __global__ void k_copy16(const float4* __restrict__ p, float4* __restrict__ q, int64_t n4, float thr) {
@@ -104,6 +112,18 @@ int main() {
         }
         printf("DPP primitives: %d mismatches\n", bad);
         if (bad) return 1;
+        // ragged buffer loads: values below len, zeros past it, for every len % 4
+        float *src, *dst; CK(hipMalloc(&src, 16384 * 4 + 64)); CK(hipMalloc(&dst, 16384 * 4));
+        std::vector<float> hsrc(16384 + 16); for (int i = 0; i < (int)hsrc.size(); ++i) hsrc[i] = 1.0f + i;
+        CK(hipMemcpy(src, hsrc.data(), hsrc.size() * 4, hipMemcpyHostToDevice));
+        int rbad = 0;
+        for (int len : {1, 2, 3, 4, 5, 6, 7, 1001, 4097, 9407, 16383}) {
+            hipLaunchKernelGGL(k_ragged_test, dim3(1), dim3(256), 0, 0, src + 3, len, dst);
+            std::vector<float> hd(16384); CK(hipMemcpy(hd.data(), dst, 16384 * 4, hipMemcpyDeviceToHost));
+            for (int i = 0; i < 16384; ++i) rbad += hd[i] != (i < len ? hsrc[i + 3] : 0.0f);
+        }
+        printf("ragged buffer loads: %d mismatches\n", rbad);
+        if (rbad) return 1;
     }
 
     const int shapes[20] = {9408, 36864, 36864, 36864, 36864, 8192, 73728, 147456, 147456, 147456, 32768, 294912,
@@ -149,60 +169,38 @@ int main() {
     };
     // full pipeline once to get state
     for (int i = t.nseg; i < SEG_PER_LAUNCH; ++i) t.blk_begin[i] = INT32_MAX;
-    auto pipeline = [&]{ launch_sample(t, sel, 0); launch_collect_select(t, sel, cand, res, thr, 0); launch_mask(t, thr, res, 0); };
+    auto pipeline = [&]{ launch_collect(t, sel, cand, 0); launch_select(t, sel, cand, res, thr, 0); launch_mask(t, thr, res, 0); };
     bench("pipeline (3 kernels)", pipeline, tot * 8.0);
     bench("copy16 contiguous", [&]{ hipLaunchKernelGGL(k_copy16, dim3((tot/4 + 4095)/4096), dim3(256), 0, 0, (float4*)cx, (float4*)cy, tot/4, 0.01f); }, tot * 8.0);
     bench("k_mask", [&]{ launch_mask(t, thr, res, 0); }, tot * 8.0);
     const int fb = (int)(tot / CHUNK);
 #define V(S, G, Z, B, nm) bench(nm, [&]{ hipLaunchKernelGGL((k_maskv<S, G, Z, B>), dim3(S ? t.nblk : fb), dim3(256), 0, 0, t, sel, res, cx, cy, 0.0015f); }, tot * 8.0);
     V(false, false, false, false, "maskv flat")
-    V(true, false, false, false, "maskv seg")
     V(true, true, true, false, "maskv seg +thrg +zc")
-    bench("k_sample", [&]{ launch_sample(t, sel, 0); }, 0);
-    bench("k_sample_t<4096>", [&]{ hipLaunchKernelGGL(k_sample_t<4096>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }, 0);
-    bench("k_sample_t<16384>", [&]{ hipLaunchKernelGGL(k_sample_t<16384>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }, 0);
-    {   // pipelines with different sample sizes
-        auto pipe = [&](auto ks) { ks(); launch_collect_select(t, sel, cand, res, thr, 0); launch_mask(t, thr, res, 0); };
-        bench("pipeline MS=4096", [&]{ pipe([&]{ hipLaunchKernelGGL(k_sample_t<4096>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }); }, tot * 8.0);
-        bench("pipeline MS=16384", [&]{ pipe([&]{ hipLaunchKernelGGL(k_sample_t<16384>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }); }, tot * 8.0);
-        std::vector<wtp_result> r1(20), r2(20);
-        pipe([&]{ hipLaunchKernelGGL(k_sample_t<4096>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }); CK(hipDeviceSynchronize());
-        CK(hipMemcpy(r1.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
-        pipe([&]{ hipLaunchKernelGGL(k_sample_t<32768>, dim3(t.nseg), dim3(1024), 0, 0, t, sel); }); CK(hipDeviceSynchronize());
-        CK(hipMemcpy(r2.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
-        int bad = 0; for (int i = 0; i < 20; ++i) bad += r1[i].thr64 != r2[i].thr64 || r1[i].zero_count != r2[i].zero_count || r1[i].path == 3;
-        printf("MS=4096 vs 32768 mismatches/fallbacks: %d\n", bad);
-    }
+    bench("k_collect+k_select", [&]{ launch_collect(t, sel, cand, 0); launch_select(t, sel, cand, res, thr, 0); }, tot * 4.0);
     {   // collect ablations (counters accumulate: the state is re-zeroed after)
-        bench("collect LAB1 counters only", [&]{ hipLaunchKernelGGL((k_collect_t<1, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
-        bench("collect LAB2 +staging", [&]{ hipLaunchKernelGGL((k_collect_t<2, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
-        CK(hipMemset(sel, 0, selb)); launch_sample(t, sel, 0); CK(hipDeviceSynchronize());
+        bench("collect LAB1 counters only", [&]{ hipLaunchKernelGGL((k_collect_t<1, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
+        bench("collect LAB2 +staging", [&]{ hipLaunchKernelGGL((k_collect_t<2, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
+        bench("collect LAB0 alone", [&]{ hipLaunchKernelGGL((k_collect_t<0, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
+        CK(hipMemset(sel, 0, selb)); CK(hipDeviceSynchronize());
     }
-    bench("k_collect+k_select", [&]{ launch_collect_select(t, sel, cand, res, thr, 0); }, tot * 4.0);
     {   // items per thread in k_collect: pipeline time and results vs the production IT
         std::vector<wtp_result> r0(20), r1(20);
         pipeline(); CK(hipDeviceSynchronize());
         CK(hipMemcpy(r0.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
-        auto run_it = [&](const char* nm, int it, auto kc) {
-            auto pipe = [&] { launch_sample(t, sel, 0); kc(); hipLaunchKernelGGL(k_select, dim3(t.nseg), dim3(SEL_THREADS), 0, 0, t, sel, cand, res, thr); launch_mask(t, thr, res, 0); };
-            char b1[64]; snprintf(b1, 64, "pipeline IT=%d", it); bench(b1, pipe, tot * 8.0);
-            char b2[64]; snprintf(b2, 64, "collect+select IT=%d", it);
-            bench(b2, [&] { kc(); hipLaunchKernelGGL(k_select, dim3(t.nseg), dim3(SEL_THREADS), 0, 0, t, sel, cand, res, thr); }, tot * 4.0);
+        auto run_it = [&](int it, auto kc) {
+            auto pipe = [&] { kc(); launch_select(t, sel, cand, res, thr, 0); launch_mask(t, thr, res, 0); };
+            char b1[64]; snprintf(b1, 64, "pipeline IT=%d (CT=%d)", it, 4096 / it); bench(b1, pipe, tot * 8.0);
             pipe(); CK(hipDeviceSynchronize());
             CK(hipMemcpy(r1.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
             int bad = 0; for (int i = 0; i < 20; ++i) bad += r0[i].thr64 != r1[i].thr64 || r0[i].zero_count != r1[i].zero_count || r1[i].path == 3;
-            printf("  %s: mismatches/fallbacks vs production %d\n", nm, bad);
+            printf("  IT=%d: mismatches/fallbacks vs production %d\n", it, bad);
         };
-        run_it("IT4", 4, [&] { hipLaunchKernelGGL((k_collect_t<0, 4>), dim3(t.nblk * 4), dim3(256), 0, 0, t, sel, cand); });
-        run_it("IT8", 8, [&] { hipLaunchKernelGGL((k_collect_t<0, 8>), dim3(t.nblk * 2), dim3(256), 0, 0, t, sel, cand); });
-        run_it("IT16", 16, [&] { hipLaunchKernelGGL((k_collect_t<0, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); });
-        // collect alone (counters accumulate; re-zeroed after)
-        bench("collect IT4 alone", [&] { hipLaunchKernelGGL((k_collect_t<0, 4>), dim3(t.nblk * 4), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
-        bench("collect IT8 alone", [&] { hipLaunchKernelGGL((k_collect_t<0, 8>), dim3(t.nblk * 2), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
-        bench("collect IT16 alone", [&] { hipLaunchKernelGGL((k_collect_t<0, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
-        bench("collect IT4 LAB1", [&] { hipLaunchKernelGGL((k_collect_t<1, 4>), dim3(t.nblk * 4), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
-        bench("collect IT4 LAB2", [&] { hipLaunchKernelGGL((k_collect_t<2, 4>), dim3(t.nblk * 4), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
-        CK(hipMemset(sel, 0, selb)); CK(hipMemset(cand, 0, 4)); launch_sample(t, sel, 0); CK(hipDeviceSynchronize());
+        run_it(4, [&] { hipLaunchKernelGGL((k_collect_t<0, 1024, 4>), dim3(t.nblk), dim3(1024), 0, 0, t, sel, cand); });
+        run_it(8, [&] { hipLaunchKernelGGL((k_collect_t<0, 512, 8>), dim3(t.nblk), dim3(512), 0, 0, t, sel, cand); });
+        run_it(2, [&] { hipLaunchKernelGGL((k_collect_t<0, 1024, 2>), dim3(t.nblk * 2), dim3(1024), 0, 0, t, sel, cand); });
+        int nf = 0; for (int i = 0; i < 20; ++i) nf += r0[i].path == 3;
+        printf("  production fallbacks: %d\n", nf);
     }
     {
         // per-stage times of the real sequence (events between the kernels)
@@ -214,27 +212,47 @@ int main() {
             for (int r = 0; r < R; ++r) {
                 if (mode == 0) CK(hipMemsetAsync(big, r, 256 << 20));
                 else hipLaunchKernelGGL(k_copy16, dim3((tot/4 + 4095)/4096), dim3(256), 0, 0, (float4*)cx, (float4*)cy, tot/4, 0.01f);
-                CK(hipEventRecord(ev[0])); launch_sample(t, sel, 0);
-                CK(hipEventRecord(ev[1])); launch_collect_select(t, sel, cand, res, thr, 0);
+                CK(hipEventRecord(ev[0])); launch_collect(t, sel, cand, 0);
+                CK(hipEventRecord(ev[1])); launch_select(t, sel, cand, res, thr, 0);
                 CK(hipEventRecord(ev[2])); launch_mask(t, thr, res, 0);
                 CK(hipEventRecord(ev[3])); CK(hipEventSynchronize(ev[3]));
                 for (int i = 0; i < 3; ++i) { float ms; CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1])); acc[i] += ms * 1e3; }
             }
-            printf("stages (%s): sample %.2f collect+select %.2f mask %.2f us\n", mode ? "warm" : "after 256MB memset", acc[0]/R, acc[1]/R, acc[2]/R);
+            printf("stages (%s): collect %.2f select %.2f mask %.2f us\n", mode ? "warm" : "after 256MB memset", acc[0]/R, acc[1]/R, acc[2]/R);
         }
         std::vector<SelState> hs(20);
-        hipLaunchKernelGGL(k_sample_t<M_SAMPLE>, dim3(t.nseg), dim3(1024), 0, 0, t, sel);
-        hipLaunchKernelGGL((k_collect_t<2, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand);
+        hipLaunchKernelGGL((k_collect_t<2, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand);
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(hs.data(), sel, 20 * sizeof(SelState), hipMemcpyDeviceToHost));
         for (int i = 0; i < 20; i += 3) { unsigned long long bl = 0; for (int q = 0; q < NSHARD; ++q) bl += hs[i].below[q];
             printf("  seg %2d n %8d below %8llu sh %u ovf %u kl %08x kh %08x\n", i, shapes[i], bl, hs[i].shift, hs[i].overflow, hs[i].kl, hs[i].kh); }
         CK(hipMemset(sel, 0, selb)); CK(hipDeviceSynchronize());
     }
+    {   // collect phase timeline (100 MHz wall clock): per-phase distribution over blocks
+        CK(hipMemset(sel, 0, selb));
+        unsigned long long zero[1024][8] = {}; CK(hipMemcpyToSymbol(HIP_SYMBOL(g_cprobe), zero, sizeof(zero)));
+        launch_collect(t, sel, cand, 0); CK(hipDeviceSynchronize());
+        static unsigned long long cp[1024][8];
+        CK(hipMemcpyFromSymbol(cp, HIP_SYMBOL(g_cprobe), sizeof(cp)));
+        const int nb = std::min(t.nblk, 1024);
+        unsigned long long t0 = ~0ull, tend = 0; for (int b = 0; b < nb; ++b) { t0 = std::min(t0, cp[b][0]); tend = std::max(tend, cp[b][5]); }
+        printf("  collect span (first start -> last end) %.2f us over %d blocks\n", (tend - t0) / 100.0, nb);
+        for (int k = 0; k < 6; ++k) {
+            std::vector<double> v; for (int b = 0; b < nb; ++b) if (cp[b][k]) v.push_back((cp[b][k] - t0) / 100.0);
+            std::sort(v.begin(), v.end());
+            if (v.empty()) continue;
+            printf("  probe %d: n %4zu  min %6.2f  p50 %6.2f  p90 %6.2f  max %6.2f us\n", k, v.size(), v[0], v[v.size() / 2], v[v.size() * 9 / 10], v.back());
+        }
+        std::vector<double> d[5];
+        for (int b = 0; b < nb; ++b) for (int k = 0; k < 5; ++k) if (cp[b][k] && cp[b][k + 1]) d[k].push_back((cp[b][k + 1] - cp[b][k]) / 100.0);
+        for (int k = 0; k < 5; ++k) { auto& v = d[k]; if (v.empty()) continue; std::sort(v.begin(), v.end());
+            printf("  phase %d->%d: p50 %5.2f  p90 %5.2f  max %5.2f us\n", k, k + 1, v[v.size() / 2], v[v.size() * 9 / 10], v.back()); }
+        launch_select(t, sel, cand, res, thr, 0); CK(hipDeviceSynchronize());
+    }
     {   // select phase timeline (100 MHz wall clock, per segment)
-        launch_sample(t, sel, 0); hipLaunchKernelGGL((k_collect_t<0, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand);
+        launch_collect(t, sel, cand, 0);
         CK(hipDeviceSynchronize());
-        hipLaunchKernelGGL(k_select, dim3(t.nseg), dim3(SEL_THREADS), 0, 0, t, sel, cand, res, thr);
+        launch_select(t, sel, cand, res, thr, 0);
         CK(hipDeviceSynchronize());
         unsigned long long hp[24][8];
         CK(hipMemcpyFromSymbol(hp, HIP_SYMBOL(g_probe), sizeof(hp)));
@@ -242,7 +260,6 @@ int main() {
         for (int i = 0; i < 20; i += 3) { printf("  select seg %2d (us from first start):", i);
             for (int k = 0; k < 7; ++k) printf(" %6.2f", hp[i][k] ? (double)(hp[i][k] - t0) / 100.0 : -1.0); printf("\n"); }
     }
-    bench("empty-ish: k_synth 1 elem", [&]{ launch_synth(cx, 1, 0, 0, 30, 0); }, 0);
     // print result info
     std::vector<wtp_result> hr(20);
     pipeline(); CK(hipDeviceSynchronize());

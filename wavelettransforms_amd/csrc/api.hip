@@ -363,9 +363,9 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         for (int i = tab.nseg; i < SEG_PER_LAUNCH; ++i) tab.blk_begin[i] = INT32_MAX;
         const bool first = g0 == 0;
         if (first) stage(1, s);
-        launch_sample(tab, sel, s);
+        launch_collect(tab, sel, cand, s);
         if (first) stage(2, s);
-        launch_collect_select(tab, sel, cand, results, thr_t, s);
+        launch_select(tab, sel, cand, results, thr_t, s);
         if (first) stage(3, s);
         launch_mask(tab, thr_t, results, s);
         if (first) stage(4, s);

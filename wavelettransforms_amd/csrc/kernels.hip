@@ -4,10 +4,11 @@
  * Selection (np.percentile(np.abs(coeff_arr), pct) + np.where(|c| < thr, 0, c),
  * ResNet/dwt_pruning.py:25-32) over grouped segments, one segment per tensor, on the float32
  * bit pattern of |x| (a key monotone in |x|; NaN sorts last as in np.partition):
- *   k_sample   one block per segment: 32768 sampled keys histogrammed into 1/128-octave
- *              bins -> window [kl, kh] bracketing the order statistics r0, r0+1
- *   k_collect  stream once: count keys < kl, == kl, == kh; scatter the keys inside (kl, kh)
- *              into key-range buckets (one run per bucket per block); max key
+ *   k_collect  every block first derives its segment's window [kl, kh] (bracketing the order
+ *              statistics r0, r0+1) from the same deterministic sample of M_SAMPLE keys
+ *              histogrammed into 1/128-octave bins; then it streams its chunk once: count
+ *              keys < kl, == kl, == kh; scatter the keys inside (kl, kh) into key-range
+ *              buckets (one run per bucket per block); max key
  *   k_select   one block per segment: exact radix select of both ranks from the one or two
  *              buckets that hold them (or the whole segment if the window missed), NumPy 1.x
  *              _lerp in f64, and the exact zero count of the level-0 output from the counts
@@ -89,23 +90,35 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v
 }
 
 /* IT float4 per thread of one chunk (fully populated, 16-byte aligned) */
-template <int IT>
+template <int IT, int CT = STREAM_THREADS>
 __device__ __forceinline__ void load_chunk(const float* p, float4 (&v)[IT]) {
     const float4* p4 = reinterpret_cast<const float4*>(p);
 #pragma unroll
-    for (int it = 0; it < IT; ++it) v[it] = p4[it * STREAM_THREADS + threadIdx.x];
+    for (int it = 0; it < IT; ++it) v[it] = p4[it * CT + threadIdx.x];
 }
 
-/* the float4 part of a ragged chunk (len4 float4s), all loads issued up front */
-template <int IT>
-__device__ __forceinline__ void load_chunk_part(const float* p, int len4, float4 (&v)[IT]) {
-    const float4* p4 = reinterpret_cast<const float4*>(p);
+/* A ragged or unaligned chunk of len elements: element e of slot (it, c) is
+ * 4 * (it * STREAM_THREADS + tid) + c, as in load_chunk.  Range-checked buffer loads: every
+ * load is issued unconditionally (no per-load branch and wait) and reads 0 past len. */
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ragged_rsrc(const float* p, int len) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* base = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(base, 0, __builtin_amdgcn_readfirstlane(len * 4), 0x00020000);
+}
+template <int IT, int CT = STREAM_THREADS>
+__device__ __forceinline__ void load_chunk_ragged(const float* p, int len, float4 (&v)[IT]) {
+    const __amdgpu_buffer_rsrc_t r = ragged_rsrc(p, len);
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-        const int j = it * STREAM_THREADS + threadIdx.x;
-        v[it] = j < len4 ? p4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int e = 4 * (it * CT + (int)threadIdx.x);
+        v[it].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e, 0, 0));
+        v[it].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e + 4, 0, 0));
+        v[it].z = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e + 8, 0, 0));
+        v[it].w = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e + 12, 0, 0));
     }
 }
+__device__ __forceinline__ float f4_get(const float4& v, int c) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); }
 
 /* --------------------------------------------------------- radix select --- */
 /* Find the digit (8 bits) holding rank r in a 256-bin LDS histogram; one wave. */
@@ -125,44 +138,63 @@ __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, i
     }
 }
 
-/* --------------------------------------------------------------- k_sample --- */
-constexpr int SAMPLE_THREADS = 1024;
-constexpr int FB_PER = (NB + SAMPLE_THREADS - 1) / SAMPLE_THREADS; /* 5 bins per thread */
+/* timing probes for tools/mb/lab.hip (empty in the library) */
+#ifndef WTP_PROBE
+#define WTP_PROBE(i)
+#endif
+#ifndef WTP_CPROBE
+#define WTP_CPROBE(i)
+#endif
 
-template <int MS>
-__global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_t(SegTable t, SelState* __restrict__ sel) {
-    constexpr int SAMPLE_PER = MS / SAMPLE_THREADS;
-    __shared__ uint32_t h[FB_PER * SAMPLE_THREADS];
-    __shared__ int64_t wtot[SAMPLE_THREADS / 64];
-    __shared__ int64_t found[4]; /* bin(sa), bin(sb) */
-    const SegDesc& sd = t.s[blockIdx.x];
+/* ------------------------------------------------------------ the window --- */
+/* The selection window of a segment comes from a deterministic sample: MS keys in groups of
+ * SAMPLE_GROUP contiguous floats spread evenly over the segment (the whole segment when
+ * n <= MS).  Every block of the segment draws the same sample and so derives the same window,
+ * which lets each k_collect block compute it for itself instead of waiting for a launch. */
+template <int THREADS, int MS>
+__device__ __forceinline__ void sample_keys(const SegDesc& sd, uint32_t (&k)[MS / THREADS]) {
+    constexpr int PER = MS / THREADS;
+    const int64_t n = sd.n;
+    const bool exact = n <= MS;
+    const double step = exact ? 0.0 : (double)(n - SAMPLE_GROUP) / (double)(MS / SAMPLE_GROUP - 1);
+    /* all loads unconditional and issued before any use (indices clamped) */
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int i = j * THREADS + threadIdx.x;
+        const int64_t pos = exact ? min((int64_t)i, n - 1)
+                                  : (int64_t)((double)(i / SAMPLE_GROUP) * step) + (i % SAMPLE_GROUP);
+        k[j] = abs_key(sd.data[pos]);
+    }
+}
+
+/* LDS scratch of window_from_keys: the bin histogram plus a few words */
+template <int THREADS>
+struct WindowLds {
+    static constexpr int FBP = (NB + THREADS - 1) / THREADS; /* bins per thread */
+    uint32_t h[FBP * THREADS];
+    uint32_t wtot[THREADS / 64];
+    int found[2];
+};
+
+/* Histogram the sampled keys over the NB bins, locate the sample ranks bracketing r0 and r1
+ * (6 sigma + 24 sample ranks of margin; exact ranks for a fully sampled segment) and return
+ * the window: kl = low edge of the bin of the lower bracket (0: open), kh = high edge of the
+ * bin of the upper bracket (0xFFFFFFFF: open), and the bucket shift for nsub buckets. */
+template <int THREADS, int MS>
+__device__ __forceinline__ void window_from_keys(const SegDesc& sd, const uint32_t (&k)[MS / THREADS],
+                                                 WindowLds<THREADS>& L, uint32_t* kl_out, uint32_t* kh_out,
+                                                 uint32_t* sh_out) {
+    constexpr int PER = MS / THREADS, FBP = WindowLds<THREADS>::FBP;
     const int64_t n = sd.n;
     const bool exact = n <= MS;
     const int m = exact ? (int)n : MS;
-    const float* x = sd.data;
-    /* sampled keys: groups of SAMPLE_GROUP contiguous floats spread evenly over the segment */
-    /* all loads unconditional and issued before any use (indices clamped; the sentinel marks
-     * the unused slots of a small segment) */
-    uint32_t k[SAMPLE_PER];
-    const double step = exact ? 0.0 : (double)(n - SAMPLE_GROUP) / (double)(MS / SAMPLE_GROUP - 1);
-#pragma unroll
-    for (int j = 0; j < SAMPLE_PER; ++j) {
-        const int i = j * SAMPLE_THREADS + threadIdx.x;
-        const int64_t pos = exact ? min((int64_t)i, n - 1)
-                                  : (int64_t)((double)(i / SAMPLE_GROUP) * step) + (i % SAMPLE_GROUP);
-        k[j] = abs_key(x[pos]);
-    }
-#pragma unroll
-    for (int j = 0; j < SAMPLE_PER; ++j)
-        if (j * SAMPLE_THREADS + (int)threadIdx.x >= m) k[j] = 0xFFFFFFFFu;
-    for (int i = threadIdx.x; i < FB_PER * SAMPLE_THREADS; i += SAMPLE_THREADS) h[i] = 0;
-    if (threadIdx.x < 4) found[threadIdx.x] = -1;
+    for (int i = threadIdx.x; i < FBP * THREADS; i += THREADS) L.h[i] = 0;
+    if (threadIdx.x < 2) L.found[threadIdx.x] = -1;
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < SAMPLE_PER; ++j)
-        if (k[j] != 0xFFFFFFFFu) atomicAdd(&h[key_bin(k[j])], 1u);
+    for (int j = 0; j < PER; ++j)
+        if (j * THREADS + (int)threadIdx.x < m) atomicAdd(&L.h[key_bin(k[j])], 1u);
     __syncthreads();
-    /* sample ranks bracketing r0 and r1 (exact ranks when the whole segment was sampled) */
     const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
     int64_t sa, sb;
     if (exact) {
@@ -177,44 +209,38 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_t(SegTable t, SelStat
     }
     uint32_t local = 0;
 #pragma unroll
-    for (int j = 0; j < FB_PER; ++j) local += h[threadIdx.x * FB_PER + j];
-    const int64_t incl = wave_scan_u32(local);
+    for (int j = 0; j < FBP; ++j) local += L.h[threadIdx.x * FBP + j];
+    const uint32_t incl = wave_scan_u32(local);
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 63) wtot[wv] = incl;
+    if (lane == 63) L.wtot[wv] = incl;
     __syncthreads();
-    int64_t cum = incl - (int64_t)local;
-    for (int i = 0; i < wv; ++i) cum += wtot[i];
+    int64_t cum = (int64_t)incl - local;
+    for (int i = 0; i < wv; ++i) cum += L.wtot[i];
 #pragma unroll
-    for (int j = 0; j < FB_PER; ++j) {
-        const int b = threadIdx.x * FB_PER + j;
-        const int64_t c = h[b];
+    for (int j = 0; j < FBP; ++j) {
+        const int b = threadIdx.x * FBP + j;
+        const int64_t c = L.h[b];
         if (c) {
-            if (sa >= cum && sa < cum + c) found[0] = b;
-            if (sb >= cum && sb < cum + c) found[1] = b;
+            if (sa >= cum && sa < cum + c) L.found[0] = b;
+            if (sb >= cum && sb < cum + c) L.found[1] = b;
         }
         cum += c;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        SelState& st = sel[sd.slot];
-        const uint32_t kl = (sa < 0 || found[0] < 0) ? 0u : bin_lo_key((int)found[0]);
-        const uint32_t kh = (sb >= m || found[1] < 0) ? 0xFFFFFFFFu : bin_hi_key((int)found[1]);
-        st.kl = kl;
-        st.kh = kh;
-        uint32_t sh = 0;
-        if (kh > kl + 1) {
-            const uint32_t R = kh - kl - 1; /* inside keys: (key - kl - 1) in [0, R) */
-            const int bits = 32 - __clz(R);
-            sh = bits > sd.nsub_log2 ? bits - sd.nsub_log2 : 0;
-        }
-        st.shift = sh;
+    const int f0 = L.found[0], f1 = L.found[1];
+    const uint32_t kl = (sa < 0 || f0 < 0) ? 0u : bin_lo_key(f0);
+    const uint32_t kh = (sb >= m || f1 < 0) ? 0xFFFFFFFFu : bin_hi_key(f1);
+    uint32_t sh = 0;
+    if (kh > kl + 1) {
+        const uint32_t R = kh - kl - 1; /* inside keys: (key - kl - 1) in [0, R) */
+        const int bits = 32 - __clz(R);
+        sh = bits > sd.nsub_log2 ? bits - sd.nsub_log2 : 0;
     }
+    *kl_out = kl;
+    *kh_out = kh;
+    *sh_out = sh;
 }
 
-/* timing probes for tools/mb/lab.hip (empty in the library) */
-#ifndef WTP_PROBE
-#define WTP_PROBE(i)
-#endif
 
 /* -------------------------------------------------------------- k_collect --- */
 /* LAB: 0 = the production kernel; 1 = stop after the counters; 2 = stop after staging
@@ -222,19 +248,26 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_t(SegTable t, SelStat
  * block.  FULL: a whole 16-byte-aligned sub-chunk (unpredicated loads, so the compiler can
  * count its waits); otherwise a ragged or unaligned one.  Up to a quarter of a sub-chunk's
  * keys may fall inside the window (more: the select takes the full scan). */
-template <int IT, bool FULL, int LAB>
+template <int CT, int IT, bool FULL, int LAB>
 __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __restrict__ st,
-                                             uint32_t* __restrict__ cand, int64_t base, int len, uint32_t* lsub,
-                                             uint32_t* lbase, uint32_t* stage, uint32_t (*wred)[4], int* wtot) {
-    constexpr int SUB = IT * STREAM_THREADS * 4, STAGE_CAP = SUB / 4;
+                                             uint32_t* __restrict__ cand, int64_t base, int len, bool first,
+                                             uint32_t* lsub, uint32_t* lbase, uint32_t* stage,
+                                             WindowLds<CT>& wl, uint32_t (*wred)[4], int* wtot) {
+    constexpr int SUB = IT * CT * 4, STAGE_CAP = SUB / 4;
     const float* p = sd.data + base;
-    const int len4 = FULL ? SUB / 4 : ((sd.flags & SEG_ALIGNED) ? len >> 2 : 0);
+    /* sample loads first, then the stream loads: the window is built while the chunk arrives */
+    WTP_CPROBE(0);
+    uint32_t ks[M_SAMPLE / CT];
+    sample_keys<CT, M_SAMPLE>(sd, ks);
     float4 v[IT];
-    if (FULL) load_chunk<IT>(p, v); /* stream loads first: the window state arrives meanwhile */
-    else load_chunk_part<IT>(p, len4, v);
-    const uint32_t kl = st->kl, kh = st->kh, sh = st->shift;
+    if (FULL) load_chunk<IT, CT>(p, v);
+    else load_chunk_ragged<IT, CT>(p, len, v);
+    uint32_t kl, kh, sh;
+    window_from_keys<CT, M_SAMPLE>(sd, ks, wl, &kl, &kh, &sh);
+    WTP_CPROBE(1);
+    if (first && threadIdx.x == 0) { st->kl = kl; st->kh = kh; st->shift = sh; } /* for k_select */
     const int nsub = 1 << sd.nsub_log2;
-    for (int i = threadIdx.x; i < nsub; i += STREAM_THREADS) lsub[i] = 0;
+    for (int i = threadIdx.x; i < nsub; i += CT) lsub[i] = 0;
     uint32_t below = 0, eql = 0, eqh = 0, mx = 0;
     int cnt = 0;
     auto inside = [&](uint32_t k) { return k > kl && k < kh; };
@@ -248,12 +281,11 @@ __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __rest
     };
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-        if (FULL || it * STREAM_THREADS + (int)threadIdx.x < len4) {
-            tally(v[it].x); tally(v[it].y); tally(v[it].z); tally(v[it].w);
-        }
+        const int e = 4 * (it * CT + (int)threadIdx.x);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (FULL || e + c < len) tally(f4_get(v[it], c));
     }
-    if (!FULL)
-        for (int i = len4 * 4 + threadIdx.x; i < len; i += STREAM_THREADS) tally(p[i]);
     /* one block reduction for the counters */
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     {
@@ -264,15 +296,16 @@ __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __rest
     const int incl = (int)wave_scan_u32((uint32_t)cnt);
     if (lane == 63) wtot[wv] = incl;
     __syncthreads();
+    WTP_CPROBE(2);
     int off = incl - cnt, total = 0;
-    for (int i = 0; i < STREAM_THREADS / 64; ++i) {
+    for (int i = 0; i < CT / 64; ++i) {
         if (i < wv) off += wtot[i];
         total += wtot[i];
     }
     if (threadIdx.x == 0) {
         unsigned long long a[3] = {0, 0, 0};
         uint32_t m2 = 0;
-        for (int w = 0; w < STREAM_THREADS / 64; ++w) {
+        for (int w = 0; w < CT / 64; ++w) {
             for (int q = 0; q < 3; ++q) a[q] += wred[w][q];
             m2 = max(m2, wred[w][3]);
         }
@@ -290,38 +323,36 @@ __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __rest
         int pos = off;
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            if (FULL || it * STREAM_THREADS + (int)threadIdx.x < len4) {
-                const uint32_t k4[4] = {abs_key(v[it].x), abs_key(v[it].y), abs_key(v[it].z), abs_key(v[it].w)};
+            const int e = 4 * (it * CT + (int)threadIdx.x);
 #pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (inside(k4[c])) stage[pos++] = k4[c];
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t k = abs_key(f4_get(v[it], c));
+                if ((FULL || e + c < len) && inside(k)) stage[pos++] = k;
             }
         }
-        if (!FULL)
-            for (int i = len4 * 4 + threadIdx.x; i < len; i += STREAM_THREADS) {
-                const uint32_t k = abs_key(p[i]);
-                if (inside(k)) stage[pos++] = k;
-            }
     }
     __syncthreads();
+    WTP_CPROBE(3);
     if (LAB == 2) return;
-    for (int i = threadIdx.x; i < total; i += STREAM_THREADS) atomicAdd(&lsub[(stage[i] - kl - 1) >> sh], 1u);
+    for (int i = threadIdx.x; i < total; i += CT) atomicAdd(&lsub[(stage[i] - kl - 1) >> sh], 1u);
     __syncthreads();
     /* reserve one contiguous run per non-empty bucket (one returning atomic per bucket) */
-    for (int b = threadIdx.x; b < nsub; b += STREAM_THREADS) {
+    for (int b = threadIdx.x; b < nsub; b += CT) {
         const uint32_t c = lsub[b];
         lbase[b] = c ? atomicAdd(&st->sub[b], c) : 0u;
         lsub[b] = 0;
     }
     __syncthreads();
+    WTP_CPROBE(4);
     const int64_t bcap = sd.bucket_cap;
     uint32_t* out = cand + sd.cand_off;
-    for (int i = threadIdx.x; i < total; i += STREAM_THREADS) {
+    for (int i = threadIdx.x; i < total; i += CT) {
         const uint32_t k = stage[i];
         const uint32_t b = (k - kl - 1) >> sh;
         const uint32_t at = lbase[b] + atomicAdd(&lsub[b], 1u);
         if (at < bcap) out[(int64_t)b * bcap + at] = k; /* counted beyond capacity: the select sees it */
     }
+    WTP_CPROBE(5);
 }
 
 /* ------------------------------------------------------------- the select --- */
@@ -569,16 +600,17 @@ __device__ void select_body(const SegDesc& sd, SelState* __restrict__ st, const 
 }
 
 /* one block per sub-chunk: block b takes sub-chunk (b % SPLIT) of table block (b / SPLIT) */
-template <int LAB, int IT>
-__global__ __launch_bounds__(STREAM_THREADS) void k_collect_t(SegTable t, SelState* __restrict__ sel,
+template <int LAB, int CT, int IT>
+__global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelState* __restrict__ sel,
                                                               uint32_t* __restrict__ cand) {
-    constexpr int SUB = IT * STREAM_THREADS * 4, SPLIT = CHUNK / SUB;
+    constexpr int SUB = IT * CT * 4, SPLIT = CHUNK / SUB;
     static_assert(CHUNK % SUB == 0, "sub-chunk size");
     __shared__ uint32_t lsub[NSUB_MAX];  /* this block's keys per bucket, then the running offset */
     __shared__ uint32_t lbase[NSUB_MAX]; /* reserved start of this block's run in each bucket     */
     __shared__ uint32_t stage[SUB / 4];
-    __shared__ uint32_t wred[STREAM_THREADS / 64][4];
-    __shared__ int wtot[STREAM_THREADS / 64];
+    __shared__ WindowLds<CT> wl;
+    __shared__ uint32_t wred[CT / 64][4];
+    __shared__ int wtot[CT / 64];
     const int tb = blockIdx.x / SPLIT;
     const int si = find_seg(t, tb);
     const SegDesc& sd = t.s[si];
@@ -586,10 +618,11 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_collect_t(SegTable t, SelSta
     const int len = (int)max((int64_t)0, min((int64_t)SUB, sd.n - base));
     if (len == 0) return; /* past the end of the segment's last chunk */
     SelState* st = sel + sd.slot;
+    const bool first = base == 0;
     if ((sd.flags & SEG_ALIGNED) && len == SUB)
-        collect_body<IT, true, LAB>(sd, st, cand, base, len, lsub, lbase, stage, wred, wtot);
+        collect_body<CT, IT, true, LAB>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
     else
-        collect_body<IT, false, LAB>(sd, st, cand, base, len, lsub, lbase, stage, wred, wtot);
+        collect_body<CT, IT, false, LAB>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
 }
 
 /* k_select: one 1024-thread block per segment (separate launch: the kernel boundary is the
@@ -605,33 +638,42 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(SegTable t, SelState* __
 }
 
 /* ----------------------------------------------------------------- k_mask --- */
-/* out = where(|x| < thr, 0, x) for level-0 segments; the zero count came from k_select. */
+/* out = where(|x| < thr, 0, x) over one chunk; returns the zeros written */
 template <bool FULL>
 __device__ __forceinline__ unsigned long long mask_body(const SegDesc& sd, int64_t base, int len, float thr) {
     const float* p = sd.data + base;
     float* q = sd.out + base;
-    const int len4 = FULL ? CHUNK / 4 : ((sd.flags & SEG_ALIGNED) ? len >> 2 : 0);
     float4 v[16];
     if (FULL) load_chunk<16>(p, v);
-    else load_chunk_part<16>(p, len4, v);
+    else load_chunk_ragged<16>(p, len, v);
     unsigned long long z = 0;
     auto f = [&](float xv) {
         const float y = (fabsf(xv) < thr) ? 0.0f : xv;
         z += y == 0.0f;
         return y;
     };
-    float4* q4 = reinterpret_cast<float4*>(q);
+    if (FULL) {
+        float4* q4 = reinterpret_cast<float4*>(q);
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
-        const int j = it * STREAM_THREADS + threadIdx.x;
-        if (FULL || j < len4) {
+        for (int it = 0; it < 16; ++it) {
             float4 y;
             y.x = f(v[it].x); y.y = f(v[it].y); y.z = f(v[it].z); y.w = f(v[it].w);
-            q4[j] = y;
+            q4[it * STREAM_THREADS + threadIdx.x] = y;
+        }
+    } else {
+        /* range-checked stores: writes past len are dropped, no per-store branch */
+        const __amdgpu_buffer_rsrc_t r = ragged_rsrc(q, len);
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int e = 4 * (it * STREAM_THREADS + (int)threadIdx.x);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float y = f(f4_get(v[it], c));
+                if (e + c >= len) z -= y == 0.0f; /* the zeros read past the end */
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), r, 4 * (e + c), 0, 0);
+            }
         }
     }
-    if (!FULL)
-        for (int i = len4 * 4 + threadIdx.x; i < len; i += STREAM_THREADS) q[i] = f(p[i]);
     return z;
 }
 
@@ -785,13 +827,13 @@ static inline unsigned grid_for(int64_t total) {
     return (unsigned)g;
 }
 
-void launch_sample(const SegTable& t, SelState* sel, hipStream_t s) {
-    hipLaunchKernelGGL(k_sample_t<M_SAMPLE>, dim3(t.nseg), dim3(SAMPLE_THREADS), 0, s, t, sel);
+void launch_collect(const SegTable& t, SelState* sel, uint32_t* cand, hipStream_t s) {
+    hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT>),
+                       dim3(t.nblk * (CHUNK / (COLLECT_IT * COLLECT_THREADS * 4))), dim3(COLLECT_THREADS), 0, s, t, sel,
+                       cand);
 }
-void launch_collect_select(const SegTable& t, SelState* sel, uint32_t* cand, wtp_result* res, float* thr_out,
-                           hipStream_t s) {
-    hipLaunchKernelGGL((k_collect_t<0, COLLECT_IT>), dim3(t.nblk * (CHUNK / (COLLECT_IT * STREAM_THREADS * 4))),
-                       dim3(STREAM_THREADS), 0, s, t, sel, cand);
+void launch_select(const SegTable& t, SelState* sel, const uint32_t* cand, wtp_result* res, float* thr_out,
+                   hipStream_t s) {
     hipLaunchKernelGGL(k_select, dim3(t.nseg), dim3(SEL_THREADS), 0, s, t, sel, cand, res, thr_out);
 }
 void launch_mask(const SegTable& t, const float* thr, wtp_result* res, hipStream_t s) {

@@ -13,14 +13,15 @@
 namespace wtp {
 
 /* ---- selection: sample window + one counting/collecting pass ----
- * k_sample histograms M_SAMPLE sampled keys (the whole segment when it fits) into 4099 bins
- * of the float32 bit pattern of |x| (1/128 octave in [2^-26, 2^6), plus zero / under /
- * over bins) and sets a window [kl, kh] of bin edges that brackets the order statistics
- * r0, r0+1 with a 6-sigma binomial margin; k_collect streams the data once, counting keys
- * < kl, == kl, == kh and == 0 and scattering the keys strictly inside (kl, kh) into nsub
- * key-range buckets; k_select reads only the bucket(s) holding the two ranks and resolves
- * them exactly, or by a full radix select over the segment if the window missed. */
-constexpr int M_SAMPLE = 8192;
+ * Every k_collect block histograms the same M_SAMPLE sampled keys of its segment (the whole
+ * segment when it fits) into 4099 bins of the float32 bit pattern of |x| (1/128 octave in
+ * [2^-26, 2^6), plus zero / under / over bins) and takes a window [kl, kh] of bin edges that
+ * brackets the order statistics r0, r0+1 with a 6-sigma binomial margin; it then streams its
+ * chunk once, counting keys < kl, == kl, == kh and scattering the keys strictly inside
+ * (kl, kh) into nsub key-range buckets; k_select reads only the bucket(s) holding the two
+ * ranks and resolves them exactly, or by a full radix select over the segment if the window
+ * missed. */
+constexpr int M_SAMPLE = 4096;
 constexpr int SAMPLE_GROUP = 16;   /* contiguous keys per sample group */
 constexpr int NSUB_MAX = 1024;     /* buckets over (kl, kh): 64..1024 per segment (SegDesc) */
 constexpr int BUCKET_MAX = 8192;   /* keys per bucket (two buckets are staged in LDS)       */
@@ -50,8 +51,9 @@ __host__ __device__ __forceinline__ uint32_t bin_hi_key(int b) { /* exclusive; 0
 
 /* ---- grouped launches over segments (one segment = one selection population) ---- */
 constexpr int CHUNK = 16384;        /* elements per block in the streaming passes */
-constexpr int COLLECT_IT = 16;      /* float4 per thread in k_collect (sub-chunks of CHUNK) */
 constexpr int STREAM_THREADS = 256; /* 64 elements = 16 float4 per thread          */
+constexpr int COLLECT_THREADS = 256; /* k_collect: 4 waves per block ...             */
+constexpr int COLLECT_IT = 16;       /* ... of 16 float4 per thread: one CHUNK        */
 constexpr int SEG_PER_LAUNCH = 24;
 
 enum SegFlags : int32_t {
@@ -101,7 +103,7 @@ struct alignas(128) SelState {
     uint32_t maxkey[NSHARD];          /* atomicMax (k_collect)                               */
     uint32_t overflow;                /* a block had more inside keys than it can stage     */
     uint32_t pad0[23];
-    uint32_t kl, kh;                  /* window (k_sample); kh = 0xFFFFFFFF: unbounded       */
+    uint32_t kl, kh;                  /* window (k_collect); kh = 0xFFFFFFFF: unbounded      */
     uint32_t shift;                   /* bucket of an inside key = (key - kl - 1) >> shift   */
     int32_t mode;                     /* MODE_* chosen by the select (diagnostics)           */
     float thr32;                      /* the float32 threshold the compare uses              */
@@ -121,9 +123,9 @@ struct Taps {
 };
 
 /* ---- launchers (kernels.hip) ---- */
-void launch_sample(const SegTable& t, SelState* sel, hipStream_t s);
-void launch_collect_select(const SegTable& t, SelState* sel, uint32_t* cand, wtp_result* res, float* thr_out,
-                           hipStream_t s);
+void launch_collect(const SegTable& t, SelState* sel, uint32_t* cand, hipStream_t s);
+void launch_select(const SegTable& t, SelState* sel, const uint32_t* cand, wtp_result* res, float* thr_out,
+                   hipStream_t s);
 void launch_mask(const SegTable& t, const float* thr, wtp_result* res, hipStream_t s);
 
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
