@@ -153,18 +153,20 @@ def main():
     ms_per_step = T / K * 1e3
     value = world * n_w * K / T
 
-    # ---- per-stage device durations (HIP events on the library's stream, queue pre-filled) ----
+    # ---- per-stage device durations: HIP events the library records between its launches on
+    # the stream it runs on (wtp_set_stage_events); a spin kernel in front lets the whole call be
+    # enqueued before it runs, so the events time the device, not the host; caches stay as warm
+    # as in the timed loop (the same state rocprofv3's kernel trace of this command sees) ----
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(STAGES) + 1)]
     for e in evs:
         e.record()
     torch.cuda.synchronize()
     handles = (ctypes.c_void_p * len(evs))(*[e.cuda_event for e in evs])
-    filler = torch.empty(128 << 20, dtype=torch.float32, device=dev)
     per = {st: [] for st in STAGES}
     N.lib().wtp_set_stage_events(handles, len(evs))
     try:
         for _ in range(args.stage_reps):
-            filler.mul_(1.0)  # ~0.2 ms of device work so the whole call is enqueued before it runs
+            torch.cuda._sleep(1_000_000)  # ~0.5 ms spin on the same stream
             step()
             torch.cuda.synchronize()
             for i, st in enumerate(STAGES):

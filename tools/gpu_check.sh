@@ -16,4 +16,6 @@ echo "== bench"; timeout -k 10 600 python bench.py > "$OUT/bench_$TAG.log" 2>&1 
 tail -1 "$OUT/bench_$TAG.log"
 echo "== rocprofv3"; cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 100 --warmup 5 --no-cpu --stage-reps 5 > "$OUT/bench_prof_$TAG.log" 2>&1 || { echo rocprof failed; tail -30 "$OUT/bench_prof_$TAG.log"; exit 1; }
 find "$OUT/prof_$TAG" -name "*stats*" | head
+echo "== pmc"; cd "$ROOT" && timeout -k 10 900 bash tools/pmc_run.sh "$TAG" > "$OUT/pmc_$TAG.log" 2>&1 || { echo pmc failed; tail -20 "$OUT/pmc_$TAG.log"; exit 1; }
+python3 tools/pmc_summary.py "$OUT/pmc_$TAG" "$OUT/pmc_${TAG}_cfg2.json" "$TAG" || exit 1
 echo done

@@ -60,8 +60,9 @@ def prune_sharded(weights, wavelet, level, pct, prune_fn, group=None, device=Non
     if world > 1:
         gathered = torch.empty(world * plan.max_shard, dtype=torch.float32, device=device)
         dist.all_gather_into_tensor(gathered, flat, group=group)
-        rec_all = torch.empty((world,) + tuple(rec_t.shape), dtype=rec_t.dtype, device=device)
-        dist.all_gather_into_tensor(rec_all, rec_t, group=group)
+        rec_all = torch.empty((world * rec_t.shape[0], rec_t.shape[1]), dtype=rec_t.dtype, device=device)
+        dist.all_gather_into_tensor(rec_all, rec_t, group=group)  # concatenated along dim 0
+        rec_all = rec_all.view(world, rec_t.shape[0], rec_t.shape[1])
     else:
         gathered, rec_all = flat, rec_t.unsqueeze(0)
     rec_np = rec_all.cpu().numpy()
