@@ -226,31 +226,56 @@ int check_launch() {
 }
 
 /* forward multi-level transform of one image batch into the packed array P */
+/* pywt.wavedec2 (dwt_pruning.py:67-68) into the packed layout: one tiled launch per level
+ * (filterbank.hip) where the level is large enough, else the two per-point passes.  The
+ * approximation ping-pongs between workspace temps so no launch reads what it writes. */
 void forward(const float* in, const TPlan& p, const Taps& tp, float* P, float* tL, float* tH, float* tA,
              hipStream_t s) {
     const float* cur = in;
     for (int k = 1; k <= p.L; ++k) {
-        launch_dwt_cols(cur, p.B, p.g.R[k - 1], p.g.C[k - 1], tp, tL, tH, s);
-        launch_dwt_rows(tL, tH, p.B, p.g.R[k], p.g.C[k - 1], tp, tA, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k],
-                        k == p.L, s);
-        cur = tA;
+        const int64_t R0 = p.g.R[k - 1], C0 = p.g.C[k - 1];
+        if (fb_tiled_ok(p.B, R0, C0, tp)) {
+            float* an = (cur == tA) ? tL : tA;
+            launch_fwd_level(cur, p.B, R0, C0, tp, an, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k], k == p.L, s);
+            cur = an;
+        } else {
+            float* t0 = (cur == tL) ? tA : tL;
+            float* t1 = (cur == tH) ? tA : tH;
+            float* an = (cur == tL || cur == tH || cur == tA) ? const_cast<float*>(cur) : tA;
+            launch_dwt_cols(cur, p.B, R0, C0, tp, t0, t1, s);
+            launch_dwt_rows(t0, t1, p.B, p.g.R[k], C0, tp, an, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k],
+                            k == p.L, s);
+            cur = an;
+        }
     }
 }
-
-/* inverse from P (thresholded on load with *thr unless thr == nullptr), crop, zero count */
+/* pywt.waverec2 (dwt_pruning.py:75-77) from the packed layout, thresholding the packed
+ * coefficients as they are loaded (the np.where of :31), cropping and counting zeros on the
+ * last level (:79-88).  Same buffer discipline as forward(). */
 void inverse(const float* P, const TPlan& p, const Taps& tp, const float* thr, float* out, unsigned long long* zc,
              float* tL, float* tH, float* tA, hipStream_t s) {
+    const float* cur = nullptr; /* approximation of the level above (nullptr: the packed cA) */
     for (int k = p.L; k >= 1; --k) {
         const int64_t R = p.g.R[k], C = p.g.C[k];
         const bool fromP = k == p.L;
         const int64_t a_bs = fromP ? 0 : 4 * p.g.R[k + 1] * p.g.C[k + 1];
         const int64_t lda = fromP ? 0 : 2 * p.g.C[k + 1];
-        launch_idwt_rows(fromP ? nullptr : tA, a_bs, lda, fromP, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k], p.B, R,
-                         C, tp, thr, tL, tH, s);
-        if (k > 1)
-            launch_idwt_cols(tL, tH, p.B, R, C, tp, tA, 2 * R, 2 * C, nullptr, s);
-        else
-            launch_idwt_cols(tL, tH, p.B, R, C, tp, out, p.H, p.W, zc, s);
+        const bool final = k == 1;
+        const int64_t oH = final ? p.H : 2 * R, oW = final ? p.W : 2 * C;
+        if (fb_tiled_ok(p.B, 2 * R, 2 * C, tp)) {
+            float* y = final ? out : ((cur == tA) ? tL : tA);
+            launch_inv_level(cur, a_bs, lda, fromP, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k], p.B, R, C, tp, thr, y,
+                             oH, oW, final ? zc : nullptr, s);
+            cur = y;
+        } else {
+            float* t0 = (cur == tL) ? tA : tL;
+            float* t1 = (cur == tH) ? tA : tH;
+            launch_idwt_rows(cur, a_bs, lda, fromP, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k], p.B, R, C, tp, thr,
+                             t0, t1, s);
+            float* y = final ? out : (cur ? const_cast<float*>(cur) : tA);
+            launch_idwt_cols(t0, t1, p.B, R, C, tp, y, oH, oW, final ? zc : nullptr, s);
+            cur = y;
+        }
     }
 }
 

@@ -1,0 +1,620 @@
+/*
+ * filterbank.hip -- LDS-tiled, one-launch-per-level 2-D filter bank for gfx950.
+ *
+ * pywt.wavedec2 / waverec2 in periodization mode (ResNet/dwt_pruning.py:67-77) apply one
+ * separable level at a time: analysis along axis -2 over the whole array, then along axis -1
+ * (pywt/_multidim.py:183-191); synthesis along axis -1, then axis -2 (:288-309).  Each level
+ * here is ONE kernel: a workgroup loads an input tile plus the filter halo into LDS once
+ * (periodic / odd-length extension applied while loading), runs the first 1-D pass into LDS
+ * and the second pass straight to HBM.  Every output sample is summed in PyWavelets' exact
+ * order (csrc/wt_dwt_core.h: ascending taps in the interior, the split order at the right
+ * edge, the special first synthesis site); only where the samples come from changes, so the
+ * results are bit-identical to the two-pass kernels and to the oracle.  The two bands that
+ * share a sample (lo/hi taps, or two subbands under one tap) are carried as a float2 so the
+ * multiplies and adds issue as packed FP32 (v_pk_mul_f32 / v_pk_add_f32) -- still one
+ * rounding per multiply and per add, as the contract requires (-ffp-contract=off).
+ *
+ * Forward tile: FR x FC outputs per subband; input tile (2 FR + F - 2) x (2 FC + F - 2).
+ * Inverse tile: IR x IC outputs; coefficient tiles (IR/2 + F/2 + 1) x (IC/2 + F/2 + 1).
+ */
+#include "wtp_internal.h"
+#include "wt_dwt_core.h"
+
+#pragma clang fp contract(off)
+
+namespace wtp {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+/* timing probes for tools/mb/fblab.hip (empty in the library) */
+#ifndef WTP_FPROBE
+#define WTP_FPROBE(i)
+#endif
+
+constexpr int FB_THREADS = 256;
+constexpr int FR = 16, FC = 64;  /* forward output tile (per subband) */
+constexpr int IR = 64, IC = 64;  /* inverse output tile */
+constexpr int FB_MAX_LDS = 64 * 1024;
+
+/* XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (blocks b and b+8
+ * share one L2), so tile t = xcd * per + b / 8 gives each XCD a contiguous run of tiles and the
+ * halos neighbouring tiles re-read come from that XCD's L2 (MI355X_MICROARCH.md, XCD placement;
+ * placement is a speed matter only, never correctness) */
+__device__ __forceinline__ int xcd_tile(int b, int n) {
+    const int per = (n + 7) / 8, x = b & 7, k = b >> 3;
+    const int full = n - 8 * (per - 1); /* XCDs that get `per` tiles; the rest get per - 1 */
+    return x < full ? x * per + k : full * per + (x - full) * (per - 1) + k;
+}
+
+__device__ __forceinline__ int ext_idx(int t, int N) { /* wt_ext_index in 32 bits */
+    const int Ne = N + (N & 1);
+    int r = t % Ne;
+    r = r < 0 ? r + Ne : r;
+    return r < N ? r : N - 1;
+}
+__device__ __forceinline__ int pmod32(int a, int m) {
+    const int r = a % m;
+    return r < 0 ? r + m : r;
+}
+
+/* analysis of one output (both bands) at site i = F/2 + 2o of a line of N samples;
+ * get(g) returns the sample at unwrapped position g (the tile already holds the extension) */
+template <int FT, class Get>
+__device__ __forceinline__ f2 ana2(int i, int N, int Frt, const float* lo, const float* hi, const Get& get) {
+    f2 acc = {0.0f, 0.0f};
+    if constexpr (FT > 0) {
+        /* every sample the output needs (positions i-j, j < F) is read into registers first,
+         * so the LDS reads issue back to back; then the sum runs in pywt's order */
+        float v[FT];
+#pragma unroll
+        for (int j = 0; j < FT; ++j) v[j] = get(i - j);
+        if (i < N) {
+#pragma unroll
+            for (int j = 0; j < FT; ++j) { const f2 t = {lo[j], hi[j]}; acc = acc + t * v[j]; }
+        } else {
+#pragma unroll
+            for (int j = FT - 1; j >= 0; --j)
+                if (i - j >= N) { const f2 t = {lo[j], hi[j]}; acc = acc + t * v[j]; }
+#pragma unroll
+            for (int j = 0; j < FT; ++j)
+                if (i - j < N) { const f2 t = {lo[j], hi[j]}; acc = acc + t * v[j]; }
+        }
+    } else {
+        const int F = Frt;
+        if (i < N) {
+            for (int j = 0; j < F; ++j) { const f2 t = {lo[j], hi[j]}; acc = acc + t * get(i - j); }
+        } else {
+            for (int j = F - 1; j >= 0; --j)
+                if (i - j >= N) { const f2 t = {lo[j], hi[j]}; acc = acc + t * get(i - j); }
+            for (int j = 0; j < F; ++j)
+                if (i - j < N) { const f2 t = {lo[j], hi[j]}; acc = acc + t * get(i - j); }
+        }
+    }
+    return acc;
+}
+
+/* ana2 for specialised filters with the samples already in registers: samp(j) is the sample
+ * at position i - j (a compile-time register index after unrolling) */
+template <int FT, class Samp>
+__device__ __forceinline__ f2 ana2_j(int i, int N, const float* lo, const float* hi, const Samp& samp) {
+    f2 acc = {0.0f, 0.0f};
+    if (__all(i < N)) { /* wave-uniform: the interior form, no predication */
+#pragma unroll
+        for (int j = 0; j < FT; ++j) { const f2 t = {lo[j], hi[j]}; acc = acc + t * samp(j); }
+    } else if (i < N) {
+#pragma unroll
+        for (int j = 0; j < FT; ++j) { const f2 t = {lo[j], hi[j]}; acc = acc + t * samp(j); }
+    } else {
+#pragma unroll
+        for (int j = FT - 1; j >= 0; --j)
+            if (i - j >= N) { const f2 t = {lo[j], hi[j]}; acc = acc + t * samp(j); }
+#pragma unroll
+        for (int j = 0; j < FT; ++j)
+            if (i - j < N) { const f2 t = {lo[j], hi[j]}; acc = acc + t * samp(j); }
+    }
+    return acc;
+}
+
+/* two analysis outputs at the same site sharing taps (e.g. the L and H rows): returns
+ * (lo.x, hi.x) in r0 and (lo.y, hi.y) in r1, each band carried packed over the two rows */
+template <int FT, class Get>
+__device__ __forceinline__ void ana2x2(int i, int N, int Frt, const float* lo, const float* hi, const Get& get,
+                                       f2& low, f2& high) {
+    f2 a = {0.0f, 0.0f}, d = {0.0f, 0.0f};
+    if constexpr (FT > 0) {
+        f2 v[FT];
+#pragma unroll
+        for (int j = 0; j < FT; ++j) v[j] = get(i - j);
+        auto term = [&](int j) { a = a + lo[j] * v[j]; d = d + hi[j] * v[j]; };
+        if (__all(i < N)) { /* wave-uniform: the interior form, no predication */
+#pragma unroll
+            for (int j = 0; j < FT; ++j) term(j);
+        } else if (i < N) {
+#pragma unroll
+            for (int j = 0; j < FT; ++j) term(j);
+        } else {
+#pragma unroll
+            for (int j = FT - 1; j >= 0; --j)
+                if (i - j >= N) term(j);
+#pragma unroll
+            for (int j = 0; j < FT; ++j)
+                if (i - j < N) term(j);
+        }
+    } else {
+        const int F = Frt;
+        auto term = [&](int j) { const f2 v = get(i - j); a = a + lo[j] * v; d = d + hi[j] * v; };
+        if (i < N) {
+            for (int j = 0; j < F; ++j) term(j);
+        } else {
+            for (int j = F - 1; j >= 0; --j)
+                if (i - j >= N) term(j);
+            for (int j = 0; j < F; ++j)
+                if (i - j < N) term(j);
+        }
+    }
+    low = a;
+    high = d;
+}
+
+/* synthesis site with an unwrapped source position: the H-even special last output n = 2N-1
+ * reads positions i - j + N (== i - j mod N), so a tile's sites increase monotonically */
+struct SiteU {
+    int i, iu, par, special;
+};
+__device__ __forceinline__ SiteU site_u(int n, int N, int F) {
+    const wt_syn_site s = wt_syn_locate(n, N, F);
+    SiteU u;
+    u.i = (int)s.i;
+    u.par = s.par;
+    u.special = s.special;
+    u.iu = u.i + ((s.special && n == 2 * N - 1) ? N : 0);
+    return u;
+}
+
+/* one synthesis pass (H terms) in wt_syn_pass's exact order; get(g) at unwrapped g = iu - j;
+ * tap(j) = rec[2j + par] for this output's parity */
+template <int FT, class T, class Tap, class Get>
+__device__ __forceinline__ T syn_pass_u(const SiteU& s, int N, int Frt, const Tap& tap, const Get& get, T acc) {
+    const int i = s.i;
+    if constexpr (FT > 0) {
+        constexpr int H = FT / 2;
+        T v[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) v[j] = get(s.iu - j);
+        if (s.special) {
+#pragma unroll
+            for (int j = H - 1; j >= 0; --j)
+                if (i - j >= 0) acc = acc + tap(j) * v[j];
+#pragma unroll
+            for (int j = 0; j < H; ++j)
+                if (i - j < 0) acc = acc + tap(j) * v[j];
+        } else if (i < N) {
+#pragma unroll
+            for (int j = 0; j < H; ++j) acc = acc + tap(j) * v[j];
+        } else {
+#pragma unroll
+            for (int j = H - 1; j >= 0; --j)
+                if (i - j >= N) acc = acc + tap(j) * v[j];
+#pragma unroll
+            for (int j = 0; j < H; ++j)
+                if (i - j < N) acc = acc + tap(j) * v[j];
+        }
+    } else {
+        const int H = Frt / 2;
+        if (s.special) {
+            for (int j = H - 1; j >= 0; --j)
+                if (i - j >= 0) acc = acc + tap(j) * get(s.iu - j);
+            for (int j = 0; j < H; ++j)
+                if (i - j < 0) acc = acc + tap(j) * get(s.iu - j);
+        } else if (i < N) {
+            for (int j = 0; j < H; ++j) acc = acc + tap(j) * get(s.iu - j);
+        } else {
+            for (int j = H - 1; j >= 0; --j)
+                if (i - j >= N) acc = acc + tap(j) * get(s.iu - j);
+            for (int j = 0; j < H; ++j)
+                if (i - j < N) acc = acc + tap(j) * get(s.iu - j);
+        }
+    }
+    return acc;
+}
+
+/* the interior form of syn_pass_u (not special, i < N): ascending taps */
+template <int FT, class T, class Tap, class Get>
+__device__ __forceinline__ T syn_pass_inner(const SiteU& s, int Frt, const Tap& tap, const Get& get, T acc) {
+    if constexpr (FT > 0) {
+        constexpr int H = FT / 2;
+        T v[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) v[j] = get(s.iu - j);
+#pragma unroll
+        for (int j = 0; j < H; ++j) acc = acc + tap(j) * v[j];
+    } else {
+        for (int j = 0; j < Frt / 2; ++j) acc = acc + tap(j) * get(s.iu - j);
+    }
+    return acc;
+}
+
+/* ------------------------------------------------------------- analysis --- */
+struct FwdArgs {
+    const float* in;
+    int64_t in_bs;       /* batch stride of the input level */
+    int R, C;            /* input level dims (row pitch C) */
+    int Ro, Co;          /* output dims per subband */
+    float* P;
+    int64_t P_bs;        /* packed image per batch item: PR * PC */
+    int PC, offR, offC;  /* level-k detail origin in the packed image */
+    float* anext;        /* (B, Ro, Co) next-level approximation; unused when last */
+    int last, tilesC, tilesR;
+};
+
+template <int FT>
+__global__ __launch_bounds__(FB_THREADS) void k_fwd_level(FwdArgs a, Taps tp) {
+    extern __shared__ float lds[];
+    const int F = FT ? FT : tp.F;
+    const int NR = 2 * FR + F - 2, NC = 2 * FC + F - 2;
+    float* T = lds;                /* NR x NC input tile */
+    float2* LH = reinterpret_cast<float2*>(lds + NR * NC); /* FR x NC: (L, H) column-pass outputs,
+                                                              even columns then odd (row-pass reads
+                                                              at stride 2 stay conflict-free) */
+    const int HALF = (NC + 1) / 2;
+    auto lhi = [&](int o, int cc) { return o * NC + (cc & 1) * HALF + (cc >> 1); };
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int tc = tile % a.tilesC, tr = (tile / a.tilesC) % a.tilesR, b = tile / (a.tilesC * a.tilesR);
+    const int o0r = tr * FR, o0c = tc * FC;
+    const int gr0 = 2 * o0r - F / 2 + 1, gc0 = 2 * o0c - F / 2 + 1;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const float* x = a.in + (int64_t)b * a.in_bs;
+    WTP_FPROBE(0);
+    /* 1. input tile with the periodic (odd: repeat-last) extension applied on load.  Rows
+     *    go by wave (row index and extension are scalar work), columns by lane (a plain add
+     *    except on edge tiles); for the specialised filters the trip counts are compile-time,
+     *    so every load of a thread is issued before the first LDS write. */
+    {
+        const bool cin = gc0 >= 0 && gc0 + NC <= a.C; /* no column extension in this tile */
+        auto rowptr = [&](int rr) {
+            const int gr = gr0 + rr;
+            return x + (int64_t)((gr >= 0 && gr < a.R) ? gr : ext_idx(gr, a.R)) * a.C;
+        };
+        auto colidx = [&](int cc) {
+            const int gc = gc0 + cc;
+            return cin ? gc : ((gc >= 0 && gc < a.C) ? gc : ext_idx(gc, a.C));
+        };
+        if constexpr (FT > 0) {
+            constexpr int NRc = 2 * FR + FT - 2, NCc = 2 * FC + FT - 2;
+            constexpr int RW = (NRc + 3) / 4, CW = (NCc + 63) / 64; /* rows per wave, column chunks */
+            int col[CW];
+#pragma unroll
+            for (int c = 0; c < CW; ++c) col[c] = colidx(min(lane + 64 * c, NCc - 1));
+            float v[RW][CW];
+#pragma unroll
+            for (int k = 0; k < RW; ++k) {
+                const float* xr = rowptr(min(wv + 4 * k, NRc - 1));
+#pragma unroll
+                for (int c = 0; c < CW; ++c) v[k][c] = xr[col[c]];
+            }
+#pragma unroll
+            for (int k = 0; k < RW; ++k)
+#pragma unroll
+                for (int c = 0; c < CW; ++c)
+                    if (wv + 4 * k < NRc && lane + 64 * c < NCc) T[(wv + 4 * k) * NCc + lane + 64 * c] = v[k][c];
+        } else {
+            for (int rr = wv; rr < NR; rr += FB_THREADS / 64) {
+                const float* xr = rowptr(rr);
+                for (int cc = lane; cc < NC; cc += 64) T[rr * NC + cc] = xr[colidx(cc)];
+            }
+        }
+    }
+    __syncthreads();
+    WTP_FPROBE(1);
+    /* 2. axis -2 analysis of every tile column: L, H for the tile's output rows */
+    const float* flo = tp.f[0];
+    const float* fhi = tp.f[1];
+    const int nrow = min(FR, a.Ro - o0r);
+    if constexpr (FT > 0) {
+        /* one tile column and FR/2 consecutive output rows per item: the column's
+         * FR + F - 2 samples are read once into registers and shared by the rows */
+        constexpr int RH = FR / 2, NV = 2 * RH + FT - 2, NCc = 2 * FC + FT - 2;
+        for (int it = threadIdx.x; it < 2 * NCc; it += FB_THREADS) {
+            const int h = it >= NCc, cc = it - h * NCc;
+            float v[NV];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) v[k] = T[(2 * RH * h + k) * NCc + cc];
+#pragma unroll
+            for (int r = 0; r < RH; ++r) {
+                const int o = RH * h + r;
+                if (o < nrow) {
+                    const int i = FT / 2 + 2 * (o0r + o);
+                    const f2 res = ana2_j<FT>(i, a.R, flo, fhi, [&](int j) { return v[2 * r + FT - 1 - j]; });
+                    LH[lhi(o, cc)] = make_float2(res.x, res.y);
+                }
+            }
+        }
+    } else {
+        for (int o = wv; o < nrow; o += FB_THREADS / 64) {
+            const int i = F / 2 + 2 * (o0r + o);
+            for (int cc = lane; cc < NC; cc += 64) {
+                const f2 r = ana2<FT>(i, a.R, F, flo, fhi, [&](int g) { return T[(g - gr0) * NC + cc]; });
+                LH[lhi(o, cc)] = make_float2(r.x, r.y);
+            }
+        }
+    }
+    __syncthreads();
+    WTP_FPROBE(2);
+    /* 3. axis -1 analysis of the L and H rows -> aa, ad, da, dd (packed layout) */
+    float* Pb = a.P + (int64_t)b * a.P_bs;
+    const int oc = o0c + lane;
+    if (lane < FC && oc < a.Co) {
+        const int i = F / 2 + 2 * oc;
+        for (int o = wv; o < nrow; o += FB_THREADS / 64) {
+            f2 low, high; /* low = (aa, da), high = (ad, dd) */
+            ana2x2<FT>(i, a.C, F, flo, fhi,
+                       [&](int g) {
+                           const float2 v = LH[lhi(o, g - gc0)];
+                           return f2{v.x, v.y};
+                       },
+                       low, high);
+            const int r = o0r + o;
+            if (a.last) Pb[(int64_t)r * a.PC + oc] = low.x;
+            else a.anext[((int64_t)b * a.Ro + r) * a.Co + oc] = low.x;
+            Pb[(int64_t)r * a.PC + a.offC + oc] = high.x;
+            Pb[(int64_t)(a.offR + r) * a.PC + oc] = low.y;
+            Pb[(int64_t)(a.offR + r) * a.PC + a.offC + oc] = high.y;
+        }
+    }
+    WTP_FPROBE(3);
+}
+
+/* ------------------------------------------------------------ synthesis --- */
+struct InvArgs {
+    const float* a;      /* approximation (B, R, C) with row pitch lda, batch stride a_bs */
+    int64_t a_bs;
+    int lda, a_from_P;   /* a_from_P: the approximation is the packed cA (thresholded) */
+    const float* P;
+    int64_t P_bs;
+    int PC, offR, offC;
+    int R, C;            /* coefficient dims of this level */
+    float* y;            /* output (B, outH, outW), row pitch outW */
+    int outH, outW;
+    const float* thr;    /* per-tensor float32 threshold applied to packed coefficients */
+    unsigned long long* zc;
+    int tilesC, tilesR;
+};
+
+template <int FT>
+__global__ __launch_bounds__(FB_THREADS) void k_inv_level(InvArgs a, Taps tp) {
+    extern __shared__ float lds[];
+    const int F = FT ? FT : tp.F;
+    const int H = F / 2;
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int tc = tile % a.tilesC, tr = (tile / a.tilesC) % a.tilesR, b = tile / (a.tilesC * a.tilesR);
+    const int n0 = tr * IR, m0 = tc * IC;
+    const int nl = min(n0 + IR, a.outH) - 1, ml = min(m0 + IC, a.outW) - 1;
+    const int r_lo = site_u(n0, a.R, F).iu - H + 1, r_hi = site_u(nl, a.R, F).iu;
+    const int c_lo = site_u(m0, a.C, F).iu - H + 1, c_hi = site_u(ml, a.C, F).iu;
+    const int NRr = r_hi - r_lo + 1, NCc = c_hi - c_lo + 1;
+    float2* Aq = reinterpret_cast<float2*>(lds);  /* (cA, cH=da) at each tile position  */
+    float2* Dq = Aq + NRr * NCc;                  /* (cV=ad, cD=dd)                     */
+    float2* LoHi = Dq + NRr * NCc;                /* NRr x IC: (lo, hi) row-pass output */
+    const float thr = a.thr ? *a.thr : 0.0f;      /* |c| < 0 never holds: no threshold  */
+    auto tl = [&](float c) { return (fabsf(c) < thr) ? 0.0f : c; };
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const float* Pb = a.P + (int64_t)b * a.P_bs;
+    const float* ab = a.a + (int64_t)b * a.a_bs;
+    /* 1. the four coefficient tiles (periodic wrap, thresholded on load); all loads of a
+     *    thread issued before the LDS writes (compile-time trip count) */
+    {
+        constexpr int NR_MAX = IR / 2 + (FT ? FT : 2) / 2 + 2, NC_MAX = IC / 2 + (FT ? FT : 2) / 2 + 2;
+        const bool inner = r_lo >= 0 && r_hi < a.R && c_lo >= 0 && c_hi < a.C;
+        auto load4 = [&](int rr, int cc, float4& q) {
+            const int r = inner ? r_lo + rr : pmod32(r_lo + rr, a.R), c = inner ? c_lo + cc : pmod32(c_lo + cc, a.C);
+            const float* prow = Pb + (int64_t)r * a.PC;
+            const float* drow = Pb + (int64_t)(a.offR + r) * a.PC;
+            const float va = a.a_from_P ? prow[c] : ab[(int64_t)r * a.lda + c];
+            q = make_float4(va, prow[a.offC + c], drow[c], drow[a.offC + c]); /* cA, cV=ad, cH=da, cD=dd */
+        };
+        auto store4 = [&](int rr, int cc, float4 q) {
+            const float va = a.a_from_P ? tl(q.x) : q.x;
+            Aq[rr * NCc + cc] = make_float2(va, tl(q.z));
+            Dq[rr * NCc + cc] = make_float2(tl(q.y), tl(q.w));
+        };
+        if (FT) {
+            constexpr int K = (NR_MAX * NC_MAX + FB_THREADS - 1) / FB_THREADS;
+            float4 q[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) { /* unconditional (clamped) loads: no per-load wait */
+                const int e = k * FB_THREADS + threadIdx.x;
+                const int rr = e / NC_MAX, cc = e - rr * NC_MAX;
+                load4(min(rr, NRr - 1), min(cc, NCc - 1), q[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int e = k * FB_THREADS + threadIdx.x;
+                const int rr = e / NC_MAX, cc = e - rr * NC_MAX;
+                if (rr < NRr && cc < NCc) store4(rr, cc, q[k]);
+            }
+        } else {
+            for (int e = threadIdx.x; e < NRr * NCc; e += FB_THREADS) {
+                const int rr = e / NCc, cc = e - rr * NCc;
+                float4 q;
+                load4(rr, cc, q);
+                store4(rr, cc, q);
+            }
+        }
+    }
+    __syncthreads();
+    /* 2. axis -1 synthesis of every tile row: lo = rec(cA, cV), hi = rec(cH, cD), carried
+     *    packed as (lo, hi): rec_lo over (cA, cH), then rec_hi over (cV, cD).  Each lane's
+     *    taps (its output parity) are resolved into registers once. */
+    const float* rlo = tp.f[2];
+    const float* rhi = tp.f[3];
+    constexpr int HM = FT ? FT / 2 : 1;
+    const int m = m0 + lane;
+    if (lane < IC && m <= ml) {
+        const SiteU s = site_u(m, a.C, F);
+        auto getA = [&](int rr) {
+            return [&, rr](int g) { const float2 v = Aq[rr * NCc + (g - c_lo)]; return f2{v.x, v.y}; };
+        };
+        auto getD = [&](int rr) {
+            return [&, rr](int g) { const float2 v = Dq[rr * NCc + (g - c_lo)]; return f2{v.x, v.y}; };
+        };
+        if (FT) {
+            float tlo[HM], thi[HM];
+#pragma unroll
+            for (int j = 0; j < HM; ++j) {
+                const float l0 = rlo[2 * j], l1 = rlo[2 * j + 1], h0 = rhi[2 * j], h1 = rhi[2 * j + 1];
+                tlo[j] = s.par ? l1 : l0;
+                thi[j] = s.par ? h1 : h0;
+            }
+            auto tl_ = [&](int j) { return tlo[j]; };
+            auto th_ = [&](int j) { return thi[j]; };
+            const bool inner = __all(!s.special && s.i < a.C);
+            for (int rr = wv; rr < NRr; rr += FB_THREADS / 64) {
+                f2 acc = {0.0f, 0.0f};
+                if (inner) {
+                    acc = syn_pass_inner<FT>(s, F, tl_, getA(rr), acc);
+                    acc = syn_pass_inner<FT>(s, F, th_, getD(rr), acc);
+                } else {
+                    acc = syn_pass_u<FT>(s, a.C, F, tl_, getA(rr), acc);
+                    acc = syn_pass_u<FT>(s, a.C, F, th_, getD(rr), acc);
+                }
+                LoHi[rr * IC + lane] = make_float2(acc.x, acc.y);
+            }
+        } else {
+            auto tl_ = [&](int j) { return rlo[2 * j + s.par]; };
+            auto th_ = [&](int j) { return rhi[2 * j + s.par]; };
+            for (int rr = wv; rr < NRr; rr += FB_THREADS / 64) {
+                f2 acc = {0.0f, 0.0f};
+                acc = syn_pass_u<FT>(s, a.C, F, tl_, getA(rr), acc);
+                acc = syn_pass_u<FT>(s, a.C, F, th_, getD(rr), acc);
+                LoHi[rr * IC + lane] = make_float2(acc.x, acc.y);
+            }
+        }
+    }
+    __syncthreads();
+    /* 3. axis -2 synthesis: y = rec_lo over lo, then rec_hi over hi, down each column (the
+     *    site of a row is wave-uniform: scalar taps) */
+    unsigned long long z = 0;
+    if (lane < IC && m <= ml) {
+        float* yb = a.y + (int64_t)b * a.outH * a.outW;
+        for (int n = n0 + wv; n <= nl; n += FB_THREADS / 64) {
+            const SiteU s = site_u(n, a.R, F);
+            auto tl_ = [&](int j) { return rlo[2 * j + s.par]; };
+            auto th_ = [&](int j) { return rhi[2 * j + s.par]; };
+            auto gl = [&](int g) { return LoHi[(g - r_lo) * IC + lane].x; };
+            auto gh = [&](int g) { return LoHi[(g - r_lo) * IC + lane].y; };
+            float acc = 0.0f;
+            if (!s.special && s.i < a.R) {
+                acc = syn_pass_inner<FT>(s, F, tl_, gl, acc);
+                acc = syn_pass_inner<FT>(s, F, th_, gh, acc);
+            } else {
+                acc = syn_pass_u<FT>(s, a.R, F, tl_, gl, acc);
+                acc = syn_pass_u<FT>(s, a.R, F, th_, gh, acc);
+            }
+            yb[(int64_t)n * a.outW + m] = acc;
+            z += acc == 0.0f;
+        }
+    }
+    if (a.zc) {
+        __shared__ unsigned long long zs;
+        if (threadIdx.x == 0) zs = 0;
+        __syncthreads();
+        if (z) atomicAdd(&zs, z);
+        __syncthreads();
+        if (threadIdx.x == 0 && zs) atomicAdd(a.zc, zs);
+    }
+}
+
+/* ------------------------------------------------------------ launchers --- */
+static size_t fwd_lds(int F) { return sizeof(float) * ((size_t)(2 * FR + F - 2) * (2 * FC + F - 2) + 2 * (size_t)FR * (2 * FC + F - 2)); }
+static size_t inv_lds(int F) {
+    const size_t nr = IR / 2 + F / 2 + 2, nc = IC / 2 + F / 2 + 2;
+    return sizeof(float) * (4 * nr * nc + 2 * nr * IC);
+}
+
+template <int FT>
+static void fwd_go(const FwdArgs& a, int B, const Taps& tp, hipStream_t s) {
+    const int grid = a.tilesC * a.tilesR * B;
+    hipLaunchKernelGGL(k_fwd_level<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F), s, a, tp);
+}
+template <int FT>
+static void inv_go(const InvArgs& a, int B, const Taps& tp, hipStream_t s) {
+    const int grid = a.tilesC * a.tilesR * B;
+    hipLaunchKernelGGL(k_inv_level<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F), s, a, tp);
+}
+
+/* The tiled path needs an even filter, the LDS budget, and images large enough that a tile
+ * is mostly useful work (tiny conv kernels keep the per-point kernels). */
+bool fb_tiled_ok(int64_t B, int64_t R, int64_t C, const Taps& tp) {
+    if ((tp.F & 1) || fwd_lds(tp.F) > FB_MAX_LDS || inv_lds(tp.F) > FB_MAX_LDS) return false;
+    if (R > (1 << 28) || C > (1 << 28) || B * R * C > ((int64_t)1 << 31)) return false;
+    return R * C >= 512; /* at least a quarter of a forward tile of outputs */
+}
+
+void launch_fwd_level(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* anext, float* P,
+                      int64_t PR, int64_t PC, int64_t offR, int64_t offC, int last, hipStream_t s) {
+    FwdArgs a;
+    a.in = in;
+    a.in_bs = R * C;
+    a.R = (int)R;
+    a.C = (int)C;
+    a.Ro = (int)((R + 1) / 2);
+    a.Co = (int)((C + 1) / 2);
+    a.P = P;
+    a.P_bs = PR * PC;
+    a.PC = (int)PC;
+    a.offR = (int)offR;
+    a.offC = (int)offC;
+    a.anext = anext;
+    a.last = last;
+    a.tilesC = (a.Co + FC - 1) / FC;
+    a.tilesR = (a.Ro + FR - 1) / FR;
+    switch (tp.F) {
+    case 2: fwd_go<2>(a, (int)B, tp, s); break;
+    case 4: fwd_go<4>(a, (int)B, tp, s); break;
+    case 6: fwd_go<6>(a, (int)B, tp, s); break;
+    case 8: fwd_go<8>(a, (int)B, tp, s); break;
+    case 10: fwd_go<10>(a, (int)B, tp, s); break;
+    case 12: fwd_go<12>(a, (int)B, tp, s); break;
+    case 16: fwd_go<16>(a, (int)B, tp, s); break;
+    case 18: fwd_go<18>(a, (int)B, tp, s); break;
+    default: fwd_go<0>(a, (int)B, tp, s); break;
+    }
+}
+
+void launch_inv_level(const float* a_src, int64_t a_bs, int64_t lda, int a_from_P, const float* P, int64_t PR,
+                      int64_t PC, int64_t offR, int64_t offC, int64_t B, int64_t R, int64_t C, const Taps& tp,
+                      const float* thr, float* y, int64_t outH, int64_t outW, unsigned long long* zc,
+                      hipStream_t s) {
+    InvArgs a;
+    a.a = a_src ? a_src : P;
+    a.a_bs = a_bs;
+    a.lda = (int)lda;
+    a.a_from_P = a_from_P;
+    a.P = P;
+    a.P_bs = PR * PC;
+    a.PC = (int)PC;
+    a.offR = (int)offR;
+    a.offC = (int)offC;
+    a.R = (int)R;
+    a.C = (int)C;
+    a.y = y;
+    a.outH = (int)outH;
+    a.outW = (int)outW;
+    a.thr = thr;
+    a.zc = zc;
+    a.tilesC = (int)((outW + IC - 1) / IC);
+    a.tilesR = (int)((outH + IR - 1) / IR);
+    switch (tp.F) {
+    case 2: inv_go<2>(a, (int)B, tp, s); break;
+    case 4: inv_go<4>(a, (int)B, tp, s); break;
+    case 6: inv_go<6>(a, (int)B, tp, s); break;
+    case 8: inv_go<8>(a, (int)B, tp, s); break;
+    case 10: inv_go<10>(a, (int)B, tp, s); break;
+    case 12: inv_go<12>(a, (int)B, tp, s); break;
+    case 16: inv_go<16>(a, (int)B, tp, s); break;
+    case 18: inv_go<18>(a, (int)B, tp, s); break;
+    default: inv_go<0>(a, (int)B, tp, s); break;
+    }
+}
+
+}  // namespace wtp

@@ -138,6 +138,14 @@ void launch_idwt_rows(const float* a, int64_t a_bs, int64_t lda, int a_from_P, c
                       const float* thr, float* lo, float* hi, hipStream_t s);
 void launch_idwt_cols(const float* lo, const float* hi, int64_t B, int64_t R, int64_t C, const Taps& tp,
                       float* y, int64_t outH, int64_t outW, unsigned long long* zero_count, hipStream_t s);
+/* filterbank.hip: one fused, LDS-tiled launch per level */
+bool fb_tiled_ok(int64_t B, int64_t R, int64_t C, const Taps& tp);
+void launch_fwd_level(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* anext, float* P,
+                      int64_t PR, int64_t PC, int64_t offR, int64_t offC, int last, hipStream_t s);
+void launch_inv_level(const float* a_src, int64_t a_bs, int64_t lda, int a_from_P, const float* P, int64_t PR,
+                      int64_t PC, int64_t offR, int64_t offC, int64_t B, int64_t R, int64_t C, const Taps& tp,
+                      const float* thr, float* y, int64_t outH, int64_t outW, unsigned long long* zc,
+                      hipStream_t s);
 void launch_copy_threshold(const float* P, float* out, int64_t n, const float* thr, unsigned long long* zc,
                            hipStream_t s);
 void launch_synth(float* out, int64_t n, uint64_t seed, uint32_t tid, int e, hipStream_t s);
