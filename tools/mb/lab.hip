@@ -3,9 +3,9 @@
 // Not part of the product.  Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off lab.hip
 #include <hip/hip_runtime.h>
 __device__ unsigned long long g_probe[24][8];
-#define WTP_PROBE(i) do { if (threadIdx.x == 0) g_probe[blockIdx.x][i] = wall_clock64(); } while (0)
+#define WTP_PROBE(i) do { if (threadIdx.x == 0 && blockIdx.x < 24) g_probe[blockIdx.x][i] = wall_clock64(); } while (0)
 __device__ unsigned long long g_cprobe[1024][8];
-#define WTP_CPROBE(i) do { if (threadIdx.x == 0 && blockIdx.x < 1024 && blockDim.x == 256) g_cprobe[blockIdx.x][i] = wall_clock64(); } while (0)
+#define WTP_CPROBE(i) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_cprobe[blockIdx.x][i] = wall_clock64(); } while (0)
 #include "../../wavelettransforms_amd/csrc/kernels.hip"
 #include <cstdio>
 #include <cstring>
@@ -136,8 +136,8 @@ int main() {
     }
     float *cx, *cy; CK(hipMalloc(&cx, tot * 4)); CK(hipMalloc(&cy, tot * 4));
     launch_synth(cx, tot, 0, 0, 30, 0);
-    size_t selb = SEG_PER_LAUNCH * sizeof(SelState);
-    SelState* sel; CK(hipMalloc(&sel, selb)); CK(hipMemset(sel, 0, selb));
+    const size_t headb = sizeof(SelHeader) + 2 * SEL_REGION;
+    SelHeader* head; CK(hipMalloc(&head, headb)); CK(hipMemset(head, 0, headb));
     uint32_t* cand; CK(hipMalloc(&cand, tot * 4));
     wtp_result* res; CK(hipMalloc(&res, 20 * sizeof(wtp_result)));
     float* thr; CK(hipMalloc(&thr, 20 * 4));
@@ -169,103 +169,53 @@ int main() {
     };
     // full pipeline once to get state
     for (int i = t.nseg; i < SEG_PER_LAUNCH; ++i) t.blk_begin[i] = INT32_MAX;
-    auto pipeline = [&]{ launch_collect(t, sel, cand, 0); launch_select(t, sel, cand, res, thr, 0); launch_mask(t, thr, res, 0); };
-    bench("pipeline (3 kernels)", pipeline, tot * 8.0);
+    auto pipeline = [&]{ launch_collect(t, head, cand, res, 0); launch_mask_select(t, head, cand, res, thr, 0); };
+    bench("pipeline (collect + mask_select)", pipeline, tot * 8.0);
     bench("copy16 contiguous", [&]{ hipLaunchKernelGGL(k_copy16, dim3((tot/4 + 4095)/4096), dim3(256), 0, 0, (float4*)cx, (float4*)cy, tot/4, 0.01f); }, tot * 8.0);
-    bench("k_mask", [&]{ launch_mask(t, thr, res, 0); }, tot * 8.0);
-    const int fb = (int)(tot / CHUNK);
-#define V(S, G, Z, B, nm) bench(nm, [&]{ hipLaunchKernelGGL((k_maskv<S, G, Z, B>), dim3(S ? t.nblk : fb), dim3(256), 0, 0, t, sel, res, cx, cy, 0.0015f); }, tot * 8.0);
-    V(false, false, false, false, "maskv flat")
-    V(true, true, true, false, "maskv seg +thrg +zc")
-    bench("k_collect+k_select", [&]{ launch_collect(t, sel, cand, 0); launch_select(t, sel, cand, res, thr, 0); }, tot * 4.0);
-    {   // collect ablations (counters accumulate: the state is re-zeroed after)
-        bench("collect LAB1 counters only", [&]{ hipLaunchKernelGGL((k_collect_t<1, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
-        bench("collect LAB2 +staging", [&]{ hipLaunchKernelGGL((k_collect_t<2, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
-        bench("collect LAB0 alone", [&]{ hipLaunchKernelGGL((k_collect_t<0, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand); }, tot * 4.0);
-        CK(hipMemset(sel, 0, selb)); CK(hipDeviceSynchronize());
-    }
-    {   // items per thread in k_collect: pipeline time and results vs the production IT
-        std::vector<wtp_result> r0(20), r1(20);
-        pipeline(); CK(hipDeviceSynchronize());
-        CK(hipMemcpy(r0.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
-        auto run_it = [&](int it, auto kc) {
-            auto pipe = [&] { kc(); launch_select(t, sel, cand, res, thr, 0); launch_mask(t, thr, res, 0); };
-            char b1[64]; snprintf(b1, 64, "pipeline IT=%d (CT=%d)", it, 4096 / it); bench(b1, pipe, tot * 8.0);
-            pipe(); CK(hipDeviceSynchronize());
-            CK(hipMemcpy(r1.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
-            int bad = 0; for (int i = 0; i < 20; ++i) bad += r0[i].thr64 != r1[i].thr64 || r0[i].zero_count != r1[i].zero_count || r1[i].path == 3;
-            printf("  IT=%d: mismatches/fallbacks vs production %d\n", it, bad);
-        };
-        run_it(4, [&] { hipLaunchKernelGGL((k_collect_t<0, 1024, 4>), dim3(t.nblk), dim3(1024), 0, 0, t, sel, cand); });
-        run_it(8, [&] { hipLaunchKernelGGL((k_collect_t<0, 512, 8>), dim3(t.nblk), dim3(512), 0, 0, t, sel, cand); });
-        run_it(2, [&] { hipLaunchKernelGGL((k_collect_t<0, 1024, 2>), dim3(t.nblk * 2), dim3(1024), 0, 0, t, sel, cand); });
-        int nf = 0; for (int i = 0; i < 20; ++i) nf += r0[i].path == 3;
-        printf("  production fallbacks: %d\n", nf);
-    }
+    bench("k_collect alone", [&]{ launch_collect(t, head, cand, res, 0); }, tot * 4.0);
+    bench("collect LAB1 counters only", [&]{ hipLaunchKernelGGL((k_collect_t<1, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, head, cand, res); }, tot * 4.0);
+    bench("collect LAB2 +staging", [&]{ hipLaunchKernelGGL((k_collect_t<2, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, head, cand, res); }, tot * 4.0);
     {
         // per-stage times of the real sequence (events between the kernels)
-        hipEvent_t ev[4]; for (auto& evx : ev) CK(hipEventCreate(&evx));
+        hipEvent_t ev[3]; for (auto& evx : ev) CK(hipEventCreate(&evx));
         float* big; CK(hipMalloc(&big, 256 << 20));
         for (int mode = 0; mode < 2; ++mode) {
-            double acc[3] = {0, 0, 0};
+            double acc[2] = {0, 0};
             const int R = 20;
             for (int r = 0; r < R; ++r) {
                 if (mode == 0) CK(hipMemsetAsync(big, r, 256 << 20));
                 else hipLaunchKernelGGL(k_copy16, dim3((tot/4 + 4095)/4096), dim3(256), 0, 0, (float4*)cx, (float4*)cy, tot/4, 0.01f);
-                CK(hipEventRecord(ev[0])); launch_collect(t, sel, cand, 0);
-                CK(hipEventRecord(ev[1])); launch_select(t, sel, cand, res, thr, 0);
-                CK(hipEventRecord(ev[2])); launch_mask(t, thr, res, 0);
-                CK(hipEventRecord(ev[3])); CK(hipEventSynchronize(ev[3]));
-                for (int i = 0; i < 3; ++i) { float ms; CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1])); acc[i] += ms * 1e3; }
+                CK(hipEventRecord(ev[0])); launch_collect(t, head, cand, res, 0);
+                CK(hipEventRecord(ev[1])); launch_mask_select(t, head, cand, res, thr, 0);
+                CK(hipEventRecord(ev[2])); CK(hipEventSynchronize(ev[2]));
+                for (int i = 0; i < 2; ++i) { float ms; CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1])); acc[i] += ms * 1e3; }
             }
-            printf("stages (%s): collect %.2f select %.2f mask %.2f us\n", mode ? "warm" : "after 256MB memset", acc[0]/R, acc[1]/R, acc[2]/R);
+            printf("stages (%s): collect %.2f mask_select %.2f us\n", mode ? "warm" : "after 256MB memset", acc[0]/R, acc[1]/R);
         }
-        std::vector<SelState> hs(20);
-        hipLaunchKernelGGL((k_collect_t<2, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, sel, cand);
-        CK(hipDeviceSynchronize());
-        CK(hipMemcpy(hs.data(), sel, 20 * sizeof(SelState), hipMemcpyDeviceToHost));
-        for (int i = 0; i < 20; i += 3) { unsigned long long bl = 0; for (int q = 0; q < NSHARD; ++q) bl += hs[i].below[q];
-            printf("  seg %2d n %8d below %8llu sh %u ovf %u kl %08x kh %08x\n", i, shapes[i], bl, hs[i].shift, hs[i].overflow, hs[i].kl, hs[i].kh); }
-        CK(hipMemset(sel, 0, selb)); CK(hipDeviceSynchronize());
     }
     {   // collect phase timeline (100 MHz wall clock): per-phase distribution over blocks
-        CK(hipMemset(sel, 0, selb));
         unsigned long long zero[1024][8] = {}; CK(hipMemcpyToSymbol(HIP_SYMBOL(g_cprobe), zero, sizeof(zero)));
-        launch_collect(t, sel, cand, 0); CK(hipDeviceSynchronize());
+        launch_collect(t, head, cand, res, 0); CK(hipDeviceSynchronize());
         static unsigned long long cp[1024][8];
         CK(hipMemcpyFromSymbol(cp, HIP_SYMBOL(g_cprobe), sizeof(cp)));
         const int nb = std::min(t.nblk, 1024);
         unsigned long long t0 = ~0ull, tend = 0; for (int b = 0; b < nb; ++b) { t0 = std::min(t0, cp[b][0]); tend = std::max(tend, cp[b][5]); }
         printf("  collect span (first start -> last end) %.2f us over %d blocks\n", (tend - t0) / 100.0, nb);
-        for (int k = 0; k < 6; ++k) {
-            std::vector<double> v; for (int b = 0; b < nb; ++b) if (cp[b][k]) v.push_back((cp[b][k] - t0) / 100.0);
-            std::sort(v.begin(), v.end());
-            if (v.empty()) continue;
-            printf("  probe %d: n %4zu  min %6.2f  p50 %6.2f  p90 %6.2f  max %6.2f us\n", k, v.size(), v[0], v[v.size() / 2], v[v.size() * 9 / 10], v.back());
-        }
         std::vector<double> d[5];
         for (int b = 0; b < nb; ++b) for (int k = 0; k < 5; ++k) if (cp[b][k] && cp[b][k + 1]) d[k].push_back((cp[b][k + 1] - cp[b][k]) / 100.0);
         for (int k = 0; k < 5; ++k) { auto& v = d[k]; if (v.empty()) continue; std::sort(v.begin(), v.end());
             printf("  phase %d->%d: p50 %5.2f  p90 %5.2f  max %5.2f us\n", k, k + 1, v[v.size() / 2], v[v.size() * 9 / 10], v.back()); }
-        launch_select(t, sel, cand, res, thr, 0); CK(hipDeviceSynchronize());
-    }
-    {   // select phase timeline (100 MHz wall clock, per segment)
-        launch_collect(t, sel, cand, 0);
-        CK(hipDeviceSynchronize());
-        launch_select(t, sel, cand, res, thr, 0);
-        CK(hipDeviceSynchronize());
+        // select timeline inside k_mask_select (blocks 0..23)
+        launch_mask_select(t, head, cand, res, thr, 0); CK(hipDeviceSynchronize());
         unsigned long long hp[24][8];
         CK(hipMemcpyFromSymbol(hp, HIP_SYMBOL(g_probe), sizeof(hp)));
-        unsigned long long t0 = ~0ull; for (int i = 0; i < 20; ++i) t0 = std::min(t0, hp[i][0]);
-        for (int i = 0; i < 20; i += 3) { printf("  select seg %2d (us from first start):", i);
-            for (int k = 0; k < 7; ++k) printf(" %6.2f", hp[i][k] ? (double)(hp[i][k] - t0) / 100.0 : -1.0); printf("\n"); }
+        for (int i = 0; i < 24; i += 4) { printf("  mask_select blk %2d select phases (us from its start):", i);
+            for (int k = 1; k < 7; ++k) printf(" %6.2f", hp[i][k] ? (double)(hp[i][k] - hp[i][0]) / 100.0 : -1.0); printf("\n"); }
     }
     // print result info
     std::vector<wtp_result> hr(20);
     pipeline(); CK(hipDeviceSynchronize());
     CK(hipMemcpy(hr.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
-    std::vector<SelState> hs(20);
-    CK(hipMemcpy(hs.data(), sel, 20 * sizeof(SelState), hipMemcpyDeviceToHost));
-    for (int i = 0; i < 20; i += 4) printf("seg %d zero %lld path %d thr %.9g kl %08x kh %08x\n", i, (long long)hr[i].zero_count, hr[i].path, hr[i].thr64, hs[i].kl, hs[i].kh);
+    for (int i = 0; i < 20; i += 4) printf("seg %d zero %lld path %d thr %.9g\n", i, (long long)hr[i].zero_count, hr[i].path, hr[i].thr64);
     return 0;
 }

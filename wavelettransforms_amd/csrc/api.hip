@@ -85,7 +85,7 @@ struct Layout {
 };
 
 /* persistent slot region: identical position and size in every layout */
-constexpr size_t PERSIST_BYTES = ((SEG_PER_LAUNCH * sizeof(SelState)) + 255) / 256 * 256;
+constexpr size_t PERSIST_BYTES = ((sizeof(SelHeader) + 2 * SEL_REGION) + 255) / 256 * 256;
 
 bool pct_ok(double pct) { return pct >= 0.0 && pct <= 100.0; }
 
@@ -340,7 +340,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     if (!ws || ws_bytes < lay.total)
         return fail(WTP_EWORKSPACE, -1, "workspace too small: need %zu bytes, got %zu", lay.total, ws_bytes);
     hipStream_t s = (hipStream_t)stream;
-    SelState* sel = reinterpret_cast<SelState*>(wsb(ws, lay.sel));
+    SelHeader* head = reinterpret_cast<SelHeader*>(wsb(ws, lay.sel));
     uint32_t* cand = reinterpret_cast<uint32_t*>(wsb(ws, lay.cand));
     float* thr_t = reinterpret_cast<float*>(wsb(ws, lay.thr));
     float* tL = reinterpret_cast<float*>(wsb(ws, lay.tmp[0]));
@@ -388,12 +388,10 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         for (int i = tab.nseg; i < SEG_PER_LAUNCH; ++i) tab.blk_begin[i] = INT32_MAX;
         const bool first = g0 == 0;
         if (first) stage(1, s);
-        launch_collect(tab, sel, cand, s);
+        launch_collect(tab, head, cand, results, s);
         if (first) stage(2, s);
-        launch_select(tab, sel, cand, results, thr_t, s);
+        launch_mask_select(tab, head, cand, results, thr_t, s);
         if (first) stage(3, s);
-        launch_mask(tab, thr_t, results, s);
-        if (first) stage(4, s);
     }
     /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2) */
     for (int t = 0; t < ntensors; ++t) {
@@ -403,7 +401,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         inverse(P, p, tp, thr_t + t, tensors[t].out,
                 reinterpret_cast<unsigned long long*>(&results[t].zero_count), tL, tH, tA, s);
     }
-    stage(5, s);
+    stage(4, s);
     return check_launch();
 }
 

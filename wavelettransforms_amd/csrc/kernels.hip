@@ -9,10 +9,11 @@
  *              histogrammed into 1/128-octave bins; then it streams its chunk once: count
  *              keys < kl, == kl, == kh; scatter the keys inside (kl, kh) into key-range
  *              buckets (one run per bucket per block); max key
- *   k_select   one block per segment: exact radix select of both ranks from the one or two
- *              buckets that hold them (or the whole segment if the window missed), NumPy 1.x
- *              _lerp in f64, and the exact zero count of the level-0 output from the counts
- *   k_mask     stream again: out = |x| < thr ? 0 : x                    (level-0 segments)
+ *   k_mask_select  stream again: every block first resolves its segment's threshold (exact
+ *              radix select of both ranks from the one or two buckets that hold them, or the
+ *              whole segment if the window missed; NumPy 1.x _lerp in f64), then writes
+ *              out = |x| < thr ? 0 : x (level-0 segments); the first
+ *              block of a segment publishes the result and the exact zero count
  * Filter bank (pywt.wavedec2 / waverec2 periodization, :67-77): separable one-level passes
  * whose every output is summed in PyWavelets' exact order (csrc/wt_dwt_core.h); the
  * inverse thresholds coefficients as it loads them and the last pass crops and counts.
@@ -265,7 +266,7 @@ __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __rest
     uint32_t kl, kh, sh;
     window_from_keys<CT, M_SAMPLE>(sd, ks, wl, &kl, &kh, &sh);
     WTP_CPROBE(1);
-    if (first && threadIdx.x == 0) { st->kl = kl; st->kh = kh; st->shift = sh; } /* for k_select */
+    if (first && threadIdx.x == 0) { st->kl = kl; st->kh = kh; st->shift = sh; } /* for the select */
     const int nsub = 1 << sd.nsub_log2;
     for (int i = threadIdx.x; i < nsub; i += CT) lsub[i] = 0;
     uint32_t below = 0, eql = 0, eqh = 0, mx = 0;
@@ -434,9 +435,9 @@ __device__ __forceinline__ void wave_find_bucket(const uint32_t* sub, int nsub, 
  * NumPy threshold and the level-0 zero count, publish the results, and leave the slot clean.
  * One block of THREADS threads; `stage` holds up to stage_cap keys in LDS. */
 template <int THREADS>
-__device__ void select_body(const SegDesc& sd, SelState* __restrict__ st, const uint32_t* __restrict__ cand,
-                            wtp_result* __restrict__ res, float* __restrict__ thr_out, uint32_t* stage,
-                            int stage_cap) {
+__device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st, const uint32_t* __restrict__ cand,
+                             wtp_result* __restrict__ res, float* __restrict__ thr_out, uint32_t* stage,
+                             int stage_cap, bool publish) {
     __shared__ int sbin[2];
     __shared__ int64_t sbefore[2];
     __shared__ uint32_t lsub[NSUB_MAX];
@@ -553,8 +554,9 @@ __device__ void select_body(const SegDesc& sd, SelState* __restrict__ st, const 
     /* level-0 segments: zeros of where(|x| < thr, 0, x) = #(key < tk) with tk = bits(thr) when
      * thr > 0, else tk = 1 (only the zeros themselves).  ka <= thr <= kb and the two ranks are
      * adjacent, so #(key < tk) = below + [tk > kl] eq_lo + before + #(staged < tk).  A NaN
-     * threshold prunes nothing: k_mask counts the zeros of the copy. */
+     * threshold prunes nothing: every k_mask_select block counts the zeros of its copy. */
     WTP_PROBE(5);
+    if (!publish) return thr32; /* block-uniform */
     int64_t zc = 0;
     if ((sd.flags & SEG_MASK) && !nan) {
         const uint32_t tk = thr32 > 0.0f ? __float_as_uint(thr32) : 1u;
@@ -573,16 +575,11 @@ __device__ void select_body(const SegDesc& sd, SelState* __restrict__ st, const 
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        st->thr32 = thr32;
-        thr_out[sd.res] = thr32; /* per tensor: read by k_mask and by the inverse transform */
-        st->key_a = ka;
-        st->key_b = kb;
-        st->mode = path;
-        st->overflow = 0; /* leave the slot clean for the next call */
+        thr_out[sd.res] = thr32; /* per tensor: read by the inverse transform */
         wtp_result& r = res[sd.res];
         r.numel = sd.numel;
         r.coeff_numel = sd.n;
-        r.zero_count = zc; /* DWT segments / NaN thresholds: a later kernel adds the zeros it writes */
+        if (zc) atomicAdd((unsigned long long*)&r.zero_count, (unsigned long long)zc); /* zeroed by k_collect */
         r.thr64 = thr;
         r.thr32_bits = __float_as_uint(thr32);
         r.max_abs_bits = mk;
@@ -590,19 +587,15 @@ __device__ void select_body(const SegDesc& sd, SelState* __restrict__ st, const 
         r.path = path;
     }
     WTP_PROBE(6);
-    for (int i = threadIdx.x; i < nsub; i += THREADS) st->sub[i] = 0;
-    if (threadIdx.x < NSHARD) {
-        st->below[threadIdx.x] = 0;
-        st->eq_lo[threadIdx.x] = 0;
-        st->eq_hi[threadIdx.x] = 0;
-        st->maxkey[threadIdx.x] = 0;
-    }
+    return thr32;
 }
 
-/* one block per sub-chunk: block b takes sub-chunk (b % SPLIT) of table block (b / SPLIT) */
+/* one block per sub-chunk: block b takes sub-chunk (b % SPLIT) of table block (b / SPLIT).
+ * The block also clears its share of the idle SelState region (the previous group's) and the
+ * zero count of its segment's result; the last block to finish flips the region parity. */
 template <int LAB, int CT, int IT>
-__global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelState* __restrict__ sel,
-                                                              uint32_t* __restrict__ cand) {
+__global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelHeader* __restrict__ head, uint32_t* __restrict__ cand,
+                                                  wtp_result* __restrict__ res) {
     constexpr int SUB = IT * CT * 4, SPLIT = CHUNK / SUB;
     static_assert(CHUNK % SUB == 0, "sub-chunk size");
     __shared__ uint32_t lsub[NSUB_MAX];  /* this block's keys per bucket, then the running offset */
@@ -611,33 +604,41 @@ __global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelState* __restri
     __shared__ WindowLds<CT> wl;
     __shared__ uint32_t wred[CT / 64][4];
     __shared__ int wtot[CT / 64];
+    const uint32_t q = head->parity;
+    {   /* clear this block's slice of the idle region */
+        uint4* idle = reinterpret_cast<uint4*>(sel_region(head, q ^ 1u));
+        constexpr int NV4 = (int)(SEL_REGION / 16);
+        const int per = (NV4 + (int)gridDim.x - 1) / (int)gridDim.x;
+        for (int i = threadIdx.x; i < per; i += CT) {
+            const int j = (int)blockIdx.x * per + i;
+            if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
     const int tb = blockIdx.x / SPLIT;
     const int si = find_seg(t, tb);
     const SegDesc& sd = t.s[si];
     const int64_t base = (int64_t)(tb - sd.blk_begin) * CHUNK + (int64_t)(blockIdx.x % SPLIT) * SUB;
     const int len = (int)max((int64_t)0, min((int64_t)SUB, sd.n - base));
-    if (len == 0) return; /* past the end of the segment's last chunk */
-    SelState* st = sel + sd.slot;
+    SelState* st = sel_region(head, q) + sd.slot;
     const bool first = base == 0;
-    if ((sd.flags & SEG_ALIGNED) && len == SUB)
-        collect_body<CT, IT, true, LAB>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
-    else
-        collect_body<CT, IT, false, LAB>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
+    if (first && threadIdx.x == 0) res[sd.res].zero_count = 0; /* k_mask_select and the inverse add */
+    if (len > 0) {
+        if ((sd.flags & SEG_ALIGNED) && len == SUB)
+            collect_body<CT, IT, true, LAB>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
+        else
+            collect_body<CT, IT, false, LAB>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
+    }
+    __syncthreads(); /* every wave has read the parity */
+    if (threadIdx.x == 0) {
+        const uint32_t d = atomicAdd(&head->done, 1u);
+        if (d == gridDim.x - 1) { /* last block: visible to the next kernel at the boundary */
+            head->done = 0;
+            head->parity = q ^ 1u;
+        }
+    }
 }
 
-/* k_select: one 1024-thread block per segment (separate launch: the kernel boundary is the
- * inter-workgroup publish of k_collect's buckets; an in-kernel last-block ticket costs an
- * agent-scope L2 write-back per block, measured slower on MI355X). */
-constexpr int SEL_THREADS = 1024, SEL_STAGE = 16384;
-__global__ __launch_bounds__(SEL_THREADS) void k_select(SegTable t, SelState* __restrict__ sel,
-                                                        const uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
-                                                        float* __restrict__ thr_out) {
-    __shared__ uint32_t stage[SEL_STAGE];
-    const SegDesc& sd = t.s[blockIdx.x];
-    select_body<SEL_THREADS>(sd, sel + sd.slot, cand, res, thr_out, stage, SEL_STAGE);
-}
-
-/* ----------------------------------------------------------------- k_mask --- */
+/* ---------------------------------------------------------- k_mask_select --- */
 /* out = where(|x| < thr, 0, x) over one chunk; returns the zeros written */
 template <bool FULL>
 __device__ __forceinline__ unsigned long long mask_body(const SegDesc& sd, int64_t base, int len, float thr) {
@@ -677,19 +678,65 @@ __device__ __forceinline__ unsigned long long mask_body(const SegDesc& sd, int64
     return z;
 }
 
-/* out = where(|x| < thr, 0, x) for level-0 segments; the zero count came from the select,
- * except for a NaN threshold (nothing pruned), where the zeros of the copy are counted here. */
-__global__ __launch_bounds__(STREAM_THREADS) void k_mask(SegTable t, const float* __restrict__ thr_t,
-                                                         wtp_result* __restrict__ res) {
+/* The select and the level-0 mask in one launch.  Every block resolves its segment's
+ * threshold itself from k_collect's counters and the one or two buckets holding the ranks
+ * (a few thousand keys, read from L2), then streams its chunk: where(|x| < thr, 0, x).  The segment's first block also computes the exact zero count and
+ * publishes the result record and the per-tensor threshold (read by the inverse transform).
+ * A DWT segment needs one select (its first block), not one per chunk. */
+constexpr int MS_STAGE = 4096;
+__global__ __launch_bounds__(STREAM_THREADS) void k_mask_select(SegTable t, const SelHeader* __restrict__ head,
+                                                                const uint32_t* __restrict__ cand,
+                                                                wtp_result* __restrict__ res,
+                                                                float* __restrict__ thr_out) {
+    __shared__ uint32_t stage[MS_STAGE];
     const int si = find_seg(t, blockIdx.x);
     const SegDesc& sd = t.s[si];
-    if (!(sd.flags & SEG_MASK)) return;
     const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * CHUNK;
+    const bool masked = (sd.flags & SEG_MASK) != 0;
+    if (!masked && base != 0) return; /* block-uniform */
     const int len = (int)min((int64_t)CHUNK, sd.n - base);
-    const float thr = thr_t[sd.res];
-    const unsigned long long z = ((sd.flags & SEG_ALIGNED) && len == CHUNK) ? mask_body<true>(sd, base, len, thr)
-                                                                            : mask_body<false>(sd, base, len, thr);
-    if (thr != thr) { /* uniform */
+    const bool full = (sd.flags & SEG_ALIGNED) && len == CHUNK;
+    /* the select first: loads return in issue order (vmcnt), so chunk loads issued ahead of
+     * the select's would only delay its round trips -- and the chunk's 64 registers would sit
+     * live through it */
+    const SelState* st = sel_region(const_cast<SelHeader*>(head), head->parity ^ 1u) + sd.slot;
+    const float thr = select_body<STREAM_THREADS>(sd, st, cand, res, thr_out, stage, MS_STAGE, base == 0);
+    if (!masked) return;
+    float4 v[16];
+    {
+        const float* p = sd.data + base;
+        if (full) load_chunk<16>(p, v);
+        else load_chunk_ragged<16>(p, len, v);
+    }
+    float* q = sd.out + base;
+    unsigned long long z = 0;
+    auto f = [&](float xv) {
+        const float y = (fabsf(xv) < thr) ? 0.0f : xv;
+        z += y == 0.0f;
+        return y;
+    };
+    if (full) {
+        float4* q4 = reinterpret_cast<float4*>(q);
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            float4 y;
+            y.x = f(v[it].x); y.y = f(v[it].y); y.z = f(v[it].z); y.w = f(v[it].w);
+            q4[it * STREAM_THREADS + threadIdx.x] = y;
+        }
+    } else {
+        const __amdgpu_buffer_rsrc_t r = ragged_rsrc(q, len);
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int e = 4 * (it * STREAM_THREADS + (int)threadIdx.x);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float y = f(f4_get(v[it], c));
+                if (e + c >= len) z -= y == 0.0f; /* the zeros read past the end */
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), r, 4 * (e + c), 0, 0);
+            }
+        }
+    }
+    if (thr != thr) { /* uniform: a NaN threshold prunes nothing, the copy's zeros are counted */
         const unsigned long long tot = block_sum_u64<STREAM_THREADS>(z);
         if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long*)&res[sd.res].zero_count, tot);
     }
@@ -827,17 +874,14 @@ static inline unsigned grid_for(int64_t total) {
     return (unsigned)g;
 }
 
-void launch_collect(const SegTable& t, SelState* sel, uint32_t* cand, hipStream_t s) {
+void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s) {
     hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT>),
-                       dim3(t.nblk * (CHUNK / (COLLECT_IT * COLLECT_THREADS * 4))), dim3(COLLECT_THREADS), 0, s, t, sel,
-                       cand);
+                       dim3(t.nblk * (CHUNK / (COLLECT_IT * COLLECT_THREADS * 4))), dim3(COLLECT_THREADS), 0, s, t,
+                       head, cand, res);
 }
-void launch_select(const SegTable& t, SelState* sel, const uint32_t* cand, wtp_result* res, float* thr_out,
-                   hipStream_t s) {
-    hipLaunchKernelGGL(k_select, dim3(t.nseg), dim3(SEL_THREADS), 0, s, t, sel, cand, res, thr_out);
-}
-void launch_mask(const SegTable& t, const float* thr, wtp_result* res, hipStream_t s) {
-    hipLaunchKernelGGL(k_mask, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, thr, res);
+void launch_mask_select(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(k_mask_select, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, head, cand, res, thr_out);
 }
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
                      hipStream_t s) {

@@ -113,6 +113,21 @@ struct alignas(128) SelState {
 };
 static_assert(sizeof(SelState) % 128 == 0 && sizeof(SelState) == 4608, "SelState layout");
 
+/* The persistent head of a workspace: two SelState regions used alternately by successive
+ * launch groups.  A group's k_collect accumulates into region `parity`, zeroes the other
+ * region (the previous group's, whose readers have finished) and its last block flips
+ * `parity`; k_mask then reads region parity ^ 1.  So no kernel has to clear state that other
+ * blocks of the same kernel may still be reading. */
+struct alignas(128) SelHeader {
+    uint32_t parity;
+    uint32_t done; /* k_collect blocks finished (last one flips parity and clears this) */
+    uint32_t pad[30];
+};
+constexpr size_t SEL_REGION = SEG_PER_LAUNCH * sizeof(SelState);
+__host__ __device__ inline SelState* sel_region(void* head, uint32_t q) {
+    return reinterpret_cast<SelState*>(reinterpret_cast<char*>(head) + sizeof(SelHeader) + (size_t)q * SEL_REGION);
+}
+
 enum SelMode : int32_t { MODE_CAND = 1, MODE_WINDOW = 2, MODE_FULL = 3 };
 
 /* filter taps as a kernel argument (scalar-loaded, uniform across the wave) */
@@ -123,10 +138,9 @@ struct Taps {
 };
 
 /* ---- launchers (kernels.hip) ---- */
-void launch_collect(const SegTable& t, SelState* sel, uint32_t* cand, hipStream_t s);
-void launch_select(const SegTable& t, SelState* sel, const uint32_t* cand, wtp_result* res, float* thr_out,
-                   hipStream_t s);
-void launch_mask(const SegTable& t, const float* thr, wtp_result* res, hipStream_t s);
+void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s);
+void launch_mask_select(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
+                        hipStream_t s);
 
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
                      hipStream_t s);
