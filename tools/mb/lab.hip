@@ -173,8 +173,34 @@ int main() {
     bench("pipeline (collect + mask_select)", pipeline, tot * 8.0);
     bench("copy16 contiguous", [&]{ hipLaunchKernelGGL(k_copy16, dim3((tot/4 + 4095)/4096), dim3(256), 0, 0, (float4*)cx, (float4*)cy, tot/4, 0.01f); }, tot * 8.0);
     bench("k_collect alone", [&]{ launch_collect(t, head, cand, res, 0); }, tot * 4.0);
-    bench("collect LAB1 counters only", [&]{ hipLaunchKernelGGL((k_collect_t<1, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, head, cand, res); }, tot * 4.0);
-    bench("collect LAB2 +staging", [&]{ hipLaunchKernelGGL((k_collect_t<2, 256, 16>), dim3(t.nblk), dim3(256), 0, 0, t, head, cand, res); }, tot * 4.0);
+    bench("k_window alone", [&]{ hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, 0, t, head); }, 0);
+    bench("pipeline inline window", [&]{ hipLaunchKernelGGL((k_collect_t<0, 256, 16, true>), dim3(t.nblk), dim3(256), 0, 0, t, head, cand, res);
+                                         launch_mask_select(t, head, cand, res, thr, 0); }, tot * 8.0);
+    bench("pipeline k_window + collect", [&]{ hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, 0, t, head);
+                                              hipLaunchKernelGGL((k_collect_t<0, 256, 16, false>), dim3(t.nblk), dim3(256), 0, 0, t, head, cand, res);
+                                              launch_mask_select(t, head, cand, res, thr, 0); }, tot * 8.0);
+    {   // collect block shapes (window from k_window): pipeline time and results vs production
+        std::vector<wtp_result> r0(20), r1(20);
+        pipeline(); CK(hipDeviceSynchronize());
+        CK(hipMemcpy(r0.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
+        auto run_shape = [&](const char* nm, auto kc) {
+            auto pipe = [&] { hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, 0, t, head); kc();
+                              launch_mask_select(t, head, cand, res, thr, 0); };
+            bench(nm, pipe, tot * 8.0);
+            pipe(); CK(hipDeviceSynchronize());
+            CK(hipMemcpy(r1.data(), res, 20 * sizeof(wtp_result), hipMemcpyDeviceToHost));
+            int bad = 0; for (int i = 0; i < 20; ++i) bad += r0[i].thr64 != r1[i].thr64 || r0[i].zero_count != r1[i].zero_count || r1[i].path == 3;
+            printf("    mismatches/fallbacks vs production %d\n", bad);
+        };
+        run_shape("pipe collect CT256 IT16", [&] { hipLaunchKernelGGL((k_collect_t<0, 256, 16, false>), dim3(t.nblk), dim3(256), 0, 0, t, head, cand, res); });
+        run_shape("pipe collect CT256 IT8", [&] { hipLaunchKernelGGL((k_collect_t<0, 256, 8, false>), dim3(t.nblk * 2), dim3(256), 0, 0, t, head, cand, res); });
+        run_shape("pipe collect CT256 IT4", [&] { hipLaunchKernelGGL((k_collect_t<0, 256, 4, false>), dim3(t.nblk * 4), dim3(256), 0, 0, t, head, cand, res); });
+        run_shape("pipe collect CT512 IT8", [&] { hipLaunchKernelGGL((k_collect_t<0, 512, 8, false>), dim3(t.nblk), dim3(512), 0, 0, t, head, cand, res); });
+        run_shape("pipe collect CT128 IT16", [&] { hipLaunchKernelGGL((k_collect_t<0, 128, 16, false>), dim3(t.nblk * 2), dim3(128), 0, 0, t, head, cand, res); });
+        run_shape("pipe collect CT1024 IT4", [&] { hipLaunchKernelGGL((k_collect_t<0, 1024, 4, false>), dim3(t.nblk), dim3(1024), 0, 0, t, head, cand, res); });
+    }
+    bench("collect LAB1 counters only", [&]{ hipLaunchKernelGGL((k_collect_t<1, 256, 16, COLLECT_WINDOW_INLINE>), dim3(t.nblk), dim3(256), 0, 0, t, head, cand, res); }, tot * 4.0);
+    bench("collect LAB2 +staging", [&]{ hipLaunchKernelGGL((k_collect_t<2, 256, 16, COLLECT_WINDOW_INLINE>), dim3(t.nblk), dim3(256), 0, 0, t, head, cand, res); }, tot * 4.0);
     {
         // per-stage times of the real sequence (events between the kernels)
         hipEvent_t ev[3]; for (auto& evx : ev) CK(hipEventCreate(&evx));

@@ -7,8 +7,8 @@
  *   k_collect  every block first derives its segment's window [kl, kh] (bracketing the order
  *              statistics r0, r0+1) from the same deterministic sample of M_SAMPLE keys
  *              histogrammed into 1/128-octave bins; then it streams its chunk once: count
- *              keys < kl, == kl, == kh; scatter the keys inside (kl, kh) into key-range
- *              buckets (one run per bucket per block); max key
+ *              keys < kl and == kl; scatter the keys inside (kl, kh] into key-range buckets
+ *              (one run per bucket per block); max key
  *   k_mask_select  stream again: every block first resolves its segment's threshold (exact
  *              radix select of both ranks from the one or two buckets that hold them, or the
  *              whole segment if the window missed; NumPy 1.x _lerp in f64), then writes
@@ -233,7 +233,7 @@ __device__ __forceinline__ void window_from_keys(const SegDesc& sd, const uint32
     const uint32_t kh = (sb >= m || f1 < 0) ? 0xFFFFFFFFu : bin_hi_key(f1);
     uint32_t sh = 0;
     if (kh > kl + 1) {
-        const uint32_t R = kh - kl - 1; /* inside keys: (key - kl - 1) in [0, R) */
+        const uint32_t R = kh - kl - 1; /* inside keys kl < key <= kh: (key - kl - 1) in [0, R] */
         const int bits = 32 - __clz(R);
         sh = bits > sd.nsub_log2 ? bits - sd.nsub_log2 : 0;
     }
@@ -244,99 +244,98 @@ __device__ __forceinline__ void window_from_keys(const SegDesc& sd, const uint32
 
 
 /* -------------------------------------------------------------- k_collect --- */
-/* LAB: 0 = the production kernel; 1 = stop after the counters; 2 = stop after staging
- * (tools/mb/lab.hip ablations).  IT float4 per thread: a sub-chunk of IT * 1024 elements per
- * block.  FULL: a whole 16-byte-aligned sub-chunk (unpredicated loads, so the compiler can
- * count its waits); otherwise a ragged or unaligned one.  Up to a quarter of a sub-chunk's
- * keys may fall inside the window (more: the select takes the full scan). */
-template <int CT, int IT, bool FULL, int LAB>
+/* LAB: 0 = the production kernel; 1 = stop after the counters; 2 = stop after the bucket
+ * histogram (tools/mb/lab.hip ablations).  IT float4 per thread: a sub-chunk of IT * CT * 4
+ * elements per block.  FULL: a whole 16-byte-aligned sub-chunk (unpredicated loads);
+ * otherwise a ragged or unaligned one (range-checked buffer loads).
+ *
+ * One pass over the chunk: per key one unsigned compare each for "below" (k < kl), "equal to
+ * kl" and "inside" (kl < k <= kh, as (k - kl - 1) < (kh - kl)), and the inside keys are staged
+ * in the thread's own LDS column (stage[i * CT + tid], conflict-free, no scan).  A thread may
+ * stage up to STG of its 4*IT keys; more sends the segment to the full-scan select. */
+constexpr int STG = 24;
+template <int CT, int IT, bool FULL, int LAB, bool WIN>
 __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __restrict__ st,
                                              uint32_t* __restrict__ cand, int64_t base, int len, bool first,
                                              uint32_t* lsub, uint32_t* lbase, uint32_t* stage,
-                                             WindowLds<CT>& wl, uint32_t (*wred)[4], int* wtot) {
-    constexpr int SUB = IT * CT * 4, STAGE_CAP = SUB / 4;
+                                             WindowLds<CT>* wl, uint32_t (*wred)[4], int* wtot) {
     const float* p = sd.data + base;
-    /* sample loads first, then the stream loads: the window is built while the chunk arrives */
     WTP_CPROBE(0);
-    uint32_t ks[M_SAMPLE / CT];
-    sample_keys<CT, M_SAMPLE>(sd, ks);
-    float4 v[IT];
-    if (FULL) load_chunk<IT, CT>(p, v);
-    else load_chunk_ragged<IT, CT>(p, len, v);
     uint32_t kl, kh, sh;
-    window_from_keys<CT, M_SAMPLE>(sd, ks, wl, &kl, &kh, &sh);
+    float4 v[IT];
+    if constexpr (WIN) {
+        /* sample loads first, then the stream loads: the window is built while the chunk arrives */
+        uint32_t ks[M_SAMPLE / CT];
+        sample_keys<CT, M_SAMPLE>(sd, ks);
+        if (FULL) load_chunk<IT, CT>(p, v);
+        else load_chunk_ragged<IT, CT>(p, len, v);
+        window_from_keys<CT, M_SAMPLE>(sd, ks, *wl, &kl, &kh, &sh);
+        if (first && threadIdx.x == 0) { st->kl = kl; st->kh = kh; st->shift = sh; } /* for the select */
+    } else {
+        /* the window came from k_window; the stream loads go out first (the window words are
+         * scalar loads, counted separately from the vector loads) */
+        if (FULL) load_chunk<IT, CT>(p, v);
+        else load_chunk_ragged<IT, CT>(p, len, v);
+        kl = st->kl;
+        kh = st->kh;
+        sh = st->shift;
+    }
     WTP_CPROBE(1);
-    if (first && threadIdx.x == 0) { st->kl = kl; st->kh = kh; st->shift = sh; } /* for the select */
     const int nsub = 1 << sd.nsub_log2;
     for (int i = threadIdx.x; i < nsub; i += CT) lsub[i] = 0;
-    uint32_t below = 0, eql = 0, eqh = 0, mx = 0;
-    int cnt = 0;
-    auto inside = [&](uint32_t k) { return k > kl && k < kh; };
-    auto tally = [&](float xv) {
-        const uint32_t k = abs_key(xv);
-        mx = max(mx, k);
-        below += k < kl;
-        eql += k == kl;
-        eqh += (k == kh) & (kh != kl);
-        cnt += inside(k);
-    };
+    const uint32_t span = kh - kl; /* >= 1 */
+    uint32_t below = 0, eql = 0, mx = 0, cnt = 0;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
         const int e = 4 * (it * CT + (int)threadIdx.x);
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-            if (FULL || e + c < len) tally(f4_get(v[it], c));
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t k = abs_key(f4_get(v[it], c));
+            const bool valid = FULL || e + c < len;
+            mx = max(mx, k); /* 0 past len: no effect */
+            below += valid && k < kl;
+            eql += valid && k == kl;
+            if (valid && k - kl - 1u < span) {
+                if (cnt < STG) stage[cnt * CT + threadIdx.x] = k;
+                ++cnt;
+            }
+        }
     }
     /* one block reduction for the counters */
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     {
-        const uint32_t r0 = wave_sum_u32(below), r1 = wave_sum_u32(eql), r2 = wave_sum_u32(eqh),
-                       r3 = wave_max_u32(mx);
+        const uint32_t r0 = wave_sum_u32(below), r1 = wave_sum_u32(eql), r2 = wave_max_u32(mx),
+                       r3 = wave_max_u32(cnt);
         if (lane == 0) { wred[wv][0] = r0; wred[wv][1] = r1; wred[wv][2] = r2; wred[wv][3] = r3; }
     }
-    const int incl = (int)wave_scan_u32((uint32_t)cnt);
-    if (lane == 63) wtot[wv] = incl;
+    const uint32_t tot_w = wave_sum_u32(cnt);
+    if (lane == 0) wtot[wv] = (int)tot_w;
     __syncthreads();
     WTP_CPROBE(2);
-    int off = incl - cnt, total = 0;
-    for (int i = 0; i < CT / 64; ++i) {
-        if (i < wv) off += wtot[i];
-        total += wtot[i];
-    }
+    int total = 0;
+    uint32_t cmax = 0;
+    for (int w = 0; w < CT / 64; ++w) { total += wtot[w]; cmax = max(cmax, wred[w][3]); }
+    const bool ovf = cmax > (uint32_t)STG;
     if (threadIdx.x == 0) {
-        unsigned long long a[3] = {0, 0, 0};
+        unsigned long long a0 = 0, a1 = 0;
         uint32_t m2 = 0;
         for (int w = 0; w < CT / 64; ++w) {
-            for (int q = 0; q < 3; ++q) a[q] += wred[w][q];
-            m2 = max(m2, wred[w][3]);
+            a0 += wred[w][0];
+            a1 += wred[w][1];
+            m2 = max(m2, wred[w][2]);
         }
         const int sh8 = blockIdx.x & (NSHARD - 1);
-        if (a[0]) atomicAdd(&st->below[sh8], a[0]);
-        if (a[1]) atomicAdd(&st->eq_lo[sh8], a[1]);
-        if (a[2]) atomicAdd(&st->eq_hi[sh8], a[2]);
+        if (a0) atomicAdd(&st->below[sh8], a0);
+        if (a1) atomicAdd(&st->eq_lo[sh8], a1);
         atomicMax(&st->maxkey[sh8], m2);
-        if (total > STAGE_CAP) atomicOr(&st->overflow, 1u);
+        if (ovf) atomicOr(&st->overflow, 1u);
     }
-    /* uniform: nothing inside the window here, or too much (the select then takes the full scan) */
-    if (LAB == 1 || total == 0 || total > STAGE_CAP) return;
-    /* stage this block's inside keys, count them per bucket */
-    if (cnt) {
-        int pos = off;
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int e = 4 * (it * CT + (int)threadIdx.x);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const uint32_t k = abs_key(f4_get(v[it], c));
-                if ((FULL || e + c < len) && inside(k)) stage[pos++] = k;
-            }
-        }
-    }
-    __syncthreads();
+    /* uniform: nothing inside the window here, or a thread overflowed (full-scan select) */
+    if (LAB == 1 || total == 0 || ovf) return;
     WTP_CPROBE(3);
-    if (LAB == 2) return;
-    for (int i = threadIdx.x; i < total; i += CT) atomicAdd(&lsub[(stage[i] - kl - 1) >> sh], 1u);
+    for (uint32_t i = 0; i < cnt; ++i) atomicAdd(&lsub[(stage[i * CT + threadIdx.x] - kl - 1) >> sh], 1u);
     __syncthreads();
+    if (LAB == 2) return;
     /* reserve one contiguous run per non-empty bucket (one returning atomic per bucket) */
     for (int b = threadIdx.x; b < nsub; b += CT) {
         const uint32_t c = lsub[b];
@@ -347,8 +346,8 @@ __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __rest
     WTP_CPROBE(4);
     const int64_t bcap = sd.bucket_cap;
     uint32_t* out = cand + sd.cand_off;
-    for (int i = threadIdx.x; i < total; i += CT) {
-        const uint32_t k = stage[i];
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const uint32_t k = stage[i * CT + threadIdx.x];
         const uint32_t b = (k - kl - 1) >> sh;
         const uint32_t at = lbase[b] + atomicAdd(&lsub[b], 1u);
         if (at < bcap) out[(int64_t)b * bcap + at] = k; /* counted beyond capacity: the select sees it */
@@ -441,7 +440,7 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
     __shared__ int sbin[2];
     __shared__ int64_t sbefore[2];
     __shared__ uint32_t lsub[NSUB_MAX];
-    __shared__ unsigned long long s_cnt[4]; /* below, eq_lo, eq_hi, inside */
+    __shared__ unsigned long long s_cnt[4]; /* below, eq_lo, eq_hi (unused: 0), inside */
     __shared__ uint32_t s_mk, s_ovf;
     const int nsub = 1 << sd.nsub_log2;
     const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
@@ -476,7 +475,7 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
     const int64_t below = (int64_t)s_cnt[0], eql = (int64_t)s_cnt[1], eqh = (int64_t)s_cnt[2];
     const int64_t ncand = (int64_t)s_cnt[3];
     uint32_t mk = s_mk;
-    /* class of a rank: 0 miss, 1 == kl, 2 inside, 3 == kh */
+    /* class of a rank: 0 miss, 1 == kl, 2 inside (kl, kh]  (eqh stays 0: keys == kh are inside) */
     auto classify = [&](int64_t r, int64_t* j) {
         if (r < below) return 0;
         r -= below;
@@ -520,7 +519,7 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
             }
             WTP_PROBE(3);
             const uint64_t lo64 = (uint64_t)kl + 1 + ((uint64_t)blo << sh);
-            const uint64_t hi64 = min((uint64_t)kh - 1, (uint64_t)kl + ((uint64_t)(bhi + 1) << sh));
+            const uint64_t hi64 = min((uint64_t)kh, (uint64_t)kl + ((uint64_t)(bhi + 1) << sh));
             uint32_t xa = 0, xb = 0;
             auto getb = [&](int64_t i) {
                 return in_lds ? stage[i] : (i < nlo ? c[(int64_t)blo * bcap + i] : c[(int64_t)bhi * bcap + i - nlo]);
@@ -590,18 +589,37 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
     return thr32;
 }
 
+/* k_window: one 1024-thread block per segment derives the window of the region k_collect is
+ * about to fill (used when the window is not computed inline by every k_collect block) */
+constexpr int WIN_THREADS = 1024;
+__global__ __launch_bounds__(WIN_THREADS) void k_window(SegTable t, SelHeader* __restrict__ head) {
+    __shared__ WindowLds<WIN_THREADS> wl;
+    const SegDesc& sd = t.s[blockIdx.x];
+    uint32_t ks[M_SAMPLE / WIN_THREADS];
+    sample_keys<WIN_THREADS, M_SAMPLE>(sd, ks);
+    uint32_t kl, kh, sh;
+    window_from_keys<WIN_THREADS, M_SAMPLE>(sd, ks, wl, &kl, &kh, &sh);
+    if (threadIdx.x == 0) {
+        SelState* st = sel_region(head, head->parity) + sd.slot;
+        st->kl = kl;
+        st->kh = kh;
+        st->shift = sh;
+    }
+}
+
 /* one block per sub-chunk: block b takes sub-chunk (b % SPLIT) of table block (b / SPLIT).
  * The block also clears its share of the idle SelState region (the previous group's) and the
  * zero count of its segment's result; the last block to finish flips the region parity. */
-template <int LAB, int CT, int IT>
+template <int LAB, int CT, int IT, bool WIN>
 __global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelHeader* __restrict__ head, uint32_t* __restrict__ cand,
                                                   wtp_result* __restrict__ res) {
     constexpr int SUB = IT * CT * 4, SPLIT = CHUNK / SUB;
     static_assert(CHUNK % SUB == 0, "sub-chunk size");
     __shared__ uint32_t lsub[NSUB_MAX];  /* this block's keys per bucket, then the running offset */
     __shared__ uint32_t lbase[NSUB_MAX]; /* reserved start of this block's run in each bucket     */
-    __shared__ uint32_t stage[SUB / 4];
-    __shared__ WindowLds<CT> wl;
+    __shared__ uint32_t stage[STG * CT];
+    __shared__ WindowLds<WIN ? CT : 64> wl_; /* only the inline window uses it */
+    WindowLds<CT>* wl = WIN ? reinterpret_cast<WindowLds<CT>*>(&wl_) : nullptr;
     __shared__ uint32_t wred[CT / 64][4];
     __shared__ int wtot[CT / 64];
     const uint32_t q = head->parity;
@@ -624,9 +642,9 @@ __global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelHeader* __restr
     if (first && threadIdx.x == 0) res[sd.res].zero_count = 0; /* k_mask_select and the inverse add */
     if (len > 0) {
         if ((sd.flags & SEG_ALIGNED) && len == SUB)
-            collect_body<CT, IT, true, LAB>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
+            collect_body<CT, IT, true, LAB, WIN>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
         else
-            collect_body<CT, IT, false, LAB>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
+            collect_body<CT, IT, false, LAB, WIN>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
     }
     __syncthreads(); /* every wave has read the parity */
     if (threadIdx.x == 0) {
@@ -875,7 +893,8 @@ static inline unsigned grid_for(int64_t total) {
 }
 
 void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s) {
-    hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT>),
+    if (!COLLECT_WINDOW_INLINE) hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, s, t, head);
+    hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT, COLLECT_WINDOW_INLINE>),
                        dim3(t.nblk * (CHUNK / (COLLECT_IT * COLLECT_THREADS * 4))), dim3(COLLECT_THREADS), 0, s, t,
                        head, cand, res);
 }

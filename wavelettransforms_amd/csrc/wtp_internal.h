@@ -17,13 +17,13 @@ namespace wtp {
  * segment when it fits) into 4099 bins of the float32 bit pattern of |x| (1/128 octave in
  * [2^-26, 2^6), plus zero / under / over bins) and takes a window [kl, kh] of bin edges that
  * brackets the order statistics r0, r0+1 with a 6-sigma binomial margin; it then streams its
- * chunk once, counting keys < kl, == kl, == kh and scattering the keys strictly inside
- * (kl, kh) into nsub key-range buckets; k_select reads only the bucket(s) holding the two
+ * chunk once, counting keys < kl and == kl and scattering the keys inside (kl, kh] into nsub
+ * key-range buckets; k_select reads only the bucket(s) holding the two
  * ranks and resolves them exactly, or by a full radix select over the segment if the window
  * missed. */
 constexpr int M_SAMPLE = 4096;
 constexpr int SAMPLE_GROUP = 16;   /* contiguous keys per sample group */
-constexpr int NSUB_MAX = 1024;     /* buckets over (kl, kh): 64..1024 per segment (SegDesc) */
+constexpr int NSUB_MAX = 1024;     /* buckets over (kl, kh]: 64..1024 per segment (SegDesc) */
 constexpr int BUCKET_MAX = 8192;   /* keys per bucket (two buckets are staged in LDS)       */
 constexpr int WIN_EXP = 32;
 constexpr int MANT_BITS = 7;
@@ -54,6 +54,7 @@ constexpr int CHUNK = 16384;        /* elements per block in the streaming passe
 constexpr int STREAM_THREADS = 256; /* 64 elements = 16 float4 per thread          */
 constexpr int COLLECT_THREADS = 256; /* k_collect: 4 waves per block ...             */
 constexpr int COLLECT_IT = 16;       /* ... of 16 float4 per thread: one CHUNK        */
+constexpr bool COLLECT_WINDOW_INLINE = false; /* window per k_collect block, or one k_window launch */
 constexpr int SEG_PER_LAUNCH = 24;
 
 enum SegFlags : int32_t {
@@ -98,7 +99,7 @@ constexpr int NSHARD = 8; /* k_collect's per-segment counters are sharded by blo
 struct alignas(128) SelState {
     unsigned long long below[NSHARD]; /* atomicAdd (k_collect): keys < kl                    */
     unsigned long long eq_lo[NSHARD]; /* keys == kl                                          */
-    unsigned long long eq_hi[NSHARD]; /* keys == kh (kh != kl)                               */
+    unsigned long long eq_hi[NSHARD]; /* unused (keys == kh are bucketed with the inside keys) */
     unsigned long long spare[NSHARD];
     uint32_t maxkey[NSHARD];          /* atomicMax (k_collect)                               */
     uint32_t overflow;                /* a block had more inside keys than it can stage     */
