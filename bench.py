@@ -28,8 +28,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "weight-coeffs/s for L5 bior3.3 DWT+thresh+IDWT; achieved HBM GB/s vs peak"
-STAGES = ["forward_dwt", "k_collect", "k_mask_select", "inverse_dwt"]
-KERNEL_OF_STAGE = {"k_collect": "k_collect_t", "k_mask_select": "k_mask_select"}
+STAGES = ["forward_dwt", "k_window", "k_collect", "k_mask_select", "inverse_dwt"]
+KERNEL_OF_STAGE = {"k_window": "k_window", "k_collect": "k_collect_t", "k_mask_select": "k_mask_select"}
 
 
 def parse():
@@ -63,7 +63,7 @@ def stage_bytes(stage, n_w, pop, has_dwt):
     """Algorithmic bytes each stage must move (4 B read of w + 4 B write of w')."""
     if stage in ("forward_dwt", "inverse_dwt") and not has_dwt:
         return 0
-    return {"forward_dwt": 4 * n_w + 4 * pop, "k_collect": 4 * pop,
+    return {"forward_dwt": 4 * n_w + 4 * pop, "k_window": 0, "k_collect": 4 * pop,
             "k_mask_select": 8 * n_w if pop == n_w else 0, "inverse_dwt": 4 * pop + 4 * n_w}[stage]
 
 

@@ -117,7 +117,7 @@ int wtp_synth_f32(float* out, int64_t n, uint64_t seed, uint32_t tensor_id, int 
 
 /* measurement hook (bench.py): hipEvent_t handles recorded on the call's stream at the stage
  * boundaries of later wtp_prune*_f32 calls on this thread -- [0] start, [1] forward DWT done,
- * [2] k_collect, [3] k_mask_select, [4] inverse DWT done (first segment group).
+ * [2] k_window, [3] k_collect, [4] k_mask_select, [5] inverse DWT done (first segment group).
  * n = 0 disables. */
 int wtp_set_stage_events(void* const* events, int n);
 

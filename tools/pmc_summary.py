@@ -17,13 +17,13 @@ import re
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_collect_t", "k_select", "k_mask", "k_dwt_cols", "k_dwt_rows", "k_idwt_rows", "k_idwt_cols",
-           "k_copy_threshold"]
+KERNELS = ["k_mask_select", "k_collect_t", "k_window", "k_fwd_level", "k_inv_level", "k_dwt_cols", "k_dwt_rows",
+           "k_idwt_rows", "k_idwt_cols", "k_copy_threshold"]
 
 
 def short(name):
-    for k in KERNELS:
-        if re.search(r"\b%s\b" % re.escape(k), name) or ("::%s" % k) in name:
+    for k in KERNELS:  # exact identifier match (k_mask_select is not k_mask)
+        if re.search(r"(?<![A-Za-z0-9_])%s(?![A-Za-z0-9_])" % re.escape(k), name):
             return k
     return None
 

@@ -388,10 +388,12 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         for (int i = tab.nseg; i < SEG_PER_LAUNCH; ++i) tab.blk_begin[i] = INT32_MAX;
         const bool first = g0 == 0;
         if (first) stage(1, s);
-        launch_collect(tab, head, cand, results, s);
+        launch_window(tab, head, s);
         if (first) stage(2, s);
-        launch_mask_select(tab, head, cand, results, thr_t, s);
+        launch_collect(tab, head, cand, results, s);
         if (first) stage(3, s);
+        launch_mask_select(tab, head, cand, results, thr_t, s);
+        if (first) stage(4, s);
     }
     /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2) */
     for (int t = 0; t < ntensors; ++t) {
@@ -401,7 +403,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         inverse(P, p, tp, thr_t + t, tensors[t].out,
                 reinterpret_cast<unsigned long long*>(&results[t].zero_count), tL, tH, tA, s);
     }
-    stage(4, s);
+    stage(5, s);
     return check_launch();
 }
 

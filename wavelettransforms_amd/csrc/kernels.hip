@@ -892,8 +892,10 @@ static inline unsigned grid_for(int64_t total) {
     return (unsigned)g;
 }
 
-void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s) {
+void launch_window(const SegTable& t, SelHeader* head, hipStream_t s) {
     if (!COLLECT_WINDOW_INLINE) hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, s, t, head);
+}
+void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s) {
     hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT, COLLECT_WINDOW_INLINE>),
                        dim3(t.nblk * (CHUNK / (COLLECT_IT * COLLECT_THREADS * 4))), dim3(COLLECT_THREADS), 0, s, t,
                        head, cand, res);

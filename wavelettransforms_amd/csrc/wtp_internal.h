@@ -139,6 +139,7 @@ struct Taps {
 };
 
 /* ---- launchers (kernels.hip) ---- */
+void launch_window(const SegTable& t, SelHeader* head, hipStream_t s);
 void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s);
 void launch_mask_select(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
                         hipStream_t s);
