@@ -115,6 +115,18 @@ int wtp_waverec2_f32(const float* packed, float* out, int64_t B, int64_t H, int6
 /* synthetic inputs (csrc/wt_synth.h): out[k] = wt_synth_value(seed, tensor_id, k, e) */
 int wtp_synth_f32(float* out, int64_t n, uint64_t seed, uint32_t tensor_id, int e, wtp_stream_t stream);
 
+/* percentage_min_pruning (ResNet/min_weight_pruning.py:66-74) for a batch of tensors (the
+ * min_weight_pruning baseline of :77-139): in every tensor zero the k = int(numel * fraction)
+ * entries of smallest |w| (flattened).  Among entries with |w| equal to the k-th smallest the
+ * lowest flat indices are pruned first (torch.topk leaves that order unspecified; counts are
+ * exact either way).  k outside [0, numel] is WTP_EARG ("selected index k out of range").
+ * out may alias in.  Results: numel, zero_count (zeros of out), thr64/thr32_bits = the k-th
+ * smallest |w| (0 when k = 0).  Workspace: wtp_min_prune_workspace_size bytes, zeroed once
+ * with wtp_workspace_init. */
+size_t wtp_min_prune_workspace_size(const wtp_tensor* tensors, int ntensors, double fraction);
+int wtp_min_prune_f32(const wtp_tensor* tensors, int ntensors, double fraction, void* workspace,
+                      size_t workspace_bytes, wtp_result* results_dev, wtp_stream_t stream);
+
 /* measurement hook (bench.py): hipEvent_t handles recorded on the call's stream at the stage
  * boundaries of later wtp_prune*_f32 calls on this thread -- [0] start, [1] forward DWT done,
  * [2] k_window, [3] k_collect, [4] k_mask_select, [5] inverse DWT done (first segment group).

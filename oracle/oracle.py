@@ -81,6 +81,7 @@ def lib():
                                      ctypes.c_int]
         L.or_synth_fill.argtypes = [f32p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32,
                                     ctypes.c_int]
+        L.or_min_prune.argtypes = [f32p, f32p, ctypes.c_int64, ctypes.c_double, i64p, f32p]
         _lib = L
     return _lib
 
@@ -223,6 +224,21 @@ def prune_batch(tensors, wavelet, level, pct, nthreads=1):
                               float(pct), res, int(nthreads))
     _check(rc, wavelet)
     return outs, [r.as_dict() for r in res]
+
+
+def min_prune(x, fraction):
+    """percentage_min_pruning (min_weight_pruning.py:66-74), ties lowest index first.
+    Returns (out, zero_count, t) with t the k-th smallest |x| (0.0 when k = 0)."""
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty_like(x)
+    z = ctypes.c_int64()
+    t = ctypes.c_float()
+    rc = lib().or_min_prune(_f32p(x.reshape(-1)) if x.size else None, _f32p(out.reshape(-1)) if x.size else None,
+                            int(x.size), float(fraction), ctypes.byref(z), ctypes.byref(t))
+    if rc == -7:
+        raise RuntimeError("selected index k out of range")
+    _check(rc)
+    return out, z.value, t.value
 
 
 def synth(shape, seed, tensor_id, e):

@@ -477,6 +477,38 @@ int or_prune_batch(int ntensors, const float* const* ins, float* const* outs, co
 }
 
 /* ------------------------------------------------------------ synthetic data --- */
+/* percentage_min_pruning (ResNet/min_weight_pruning.py:66-74): k = int(n * fraction) (C cast =
+ * Python int() truncation); zero the k entries of smallest |x|; among |x| equal to the k-th
+ * smallest the lowest indices go first (the rule the GPU path implements; torch.topk leaves it
+ * unspecified).  Returns -6 on allocation failure, -7 when k is outside [0, n]. */
+int or_min_prune(const float* in, float* out, int64_t n, double fraction, int64_t* zero_count, float* tval) {
+    const double kd = (double)n * fraction;
+    if (!(kd > -1.0 && kd < (double)n + 1.0)) return -7;
+    const int64_t k = (int64_t)kd;
+    if (out != in) memcpy(out, in, (size_t)n * sizeof(float));
+    uint32_t t = 0xFFFFFFFFu;
+    if (k > 0) {
+        uint32_t* keys = (uint32_t*)malloc((size_t)n * sizeof(uint32_t));
+        if (!keys) return -6;
+        for (int64_t i = 0; i < n; ++i) keys[i] = abs_key(in[i]);
+        t = select_kth(keys, n, k - 1);
+        free(keys);
+        int64_t below = 0;
+        for (int64_t i = 0; i < n; ++i) below += abs_key(in[i]) < t;
+        int64_t need = k - below;
+        for (int64_t i = 0; i < n; ++i) {
+            const uint32_t kk = abs_key(in[i]);
+            if (kk < t) out[i] = 0.0f;
+            else if (kk == t && need > 0) { out[i] = 0.0f; --need; }
+        }
+    }
+    int64_t z = 0;
+    for (int64_t i = 0; i < n; ++i) z += out[i] == 0.0f;
+    *zero_count = z;
+    *tval = k > 0 ? key_f(t) : 0.0f;
+    return 0;
+}
+
 void or_synth_fill(float* out, int64_t n, uint64_t seed, uint32_t tensor_id, int e) {
     for (int64_t k = 0; k < n; ++k) out[k] = wt_synth_value(seed, tensor_id, (uint64_t)k, e);
 }

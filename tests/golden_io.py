@@ -20,6 +20,12 @@ def manifest():
     return _manifest
 
 
+def reference_logs():
+    """The reference's stored pruning logs (tools/extract_reference_logs.py)."""
+    with open(os.path.join(GOLDEN, "reference_logs.json")) as fh:
+        return json.load(fh)
+
+
 def arrays():
     global _cases
     if _cases is None:

@@ -73,6 +73,8 @@ def lib():
             "wtp_waverec2_f32": ([vp, vp, i64, i64, i64, i32, i32, vp, vp, sz, vp], i32),
             "wtp_synth_f32": ([vp, i64, ctypes.c_uint64, ctypes.c_uint32, i32, vp], i32),
             "wtp_set_stage_events": ([ctypes.POINTER(ctypes.c_void_p), i32], i32),
+            "wtp_min_prune_workspace_size": ([tp, i32, f64], sz),
+            "wtp_min_prune_f32": ([tp, i32, f64, vp, sz, vp, vp], i32),
             "wtp_last_error": ([], ctypes.c_char_p),
             "wtp_last_error_tensor": ([], i32),
         }

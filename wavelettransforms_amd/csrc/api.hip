@@ -417,6 +417,116 @@ int wtp_prune_layers_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id
     return prune_impl(tensors, ntensors, wavelet_id, level, pct, ws, ws_bytes, results, stream, false);
 }
 
+/* ---------------------------------------------------------- min pruning --- */
+/* percentage_min_pruning (ResNet/min_weight_pruning.py:66-74): k = int(numel * fraction)
+ * (Python int(): truncation toward zero); torch.topk rejects k outside [0, numel]. */
+struct MinPlan {
+    std::vector<TPlan> ps;
+    std::vector<int64_t> k;
+    Layout lay;
+    size_t mp_off = 0, tie_off = 0, total = 0;
+    int nblk = 0;
+};
+
+static int plan_min(const wtp_tensor* ts, int n, double fraction, bool check_ptrs, MinPlan& m) {
+    m.ps.assign(n, TPlan());
+    m.k.assign(n, 0);
+    if (!(fraction == fraction)) return fail(WTP_EARG, -1, "cannot convert float NaN to integer");
+    for (int t = 0; t < n; ++t) {
+        const wtp_tensor& x = ts[t];
+        TPlan& p = m.ps[t];
+        if (x.ndim < 0 || x.ndim > WTP_MAX_DIMS) return fail(WTP_EARG, t, "tensor %d: ndim %d unsupported", t, x.ndim);
+        p.ndim = x.ndim;
+        p.numel = 1;
+        for (int d = 0; d < x.ndim; ++d) {
+            if (x.shape[d] < 0) return fail(WTP_EARG, t, "tensor %d: negative dimension", t);
+            p.numel *= x.shape[d];
+        }
+        if (check_ptrs && p.numel > 0 && (!x.in || !x.out)) return fail(WTP_EARG, t, "tensor %d: null pointer", t);
+        if (p.numel > (int64_t)INT32_MAX) return fail(WTP_EARG, t, "tensor %d: more than 2^31-1 elements", t);
+        const double kd = (double)p.numel * fraction; /* min_weight_pruning.py:70 */
+        if (!(kd > -1.0 && kd < (double)p.numel + 1.0))
+            return fail(WTP_EARG, t, "selected index k out of range");
+        m.k[t] = (int64_t)kd; /* C cast truncates toward zero, like int() */
+        p.pop = p.numel;
+        p.cap = p.numel ? cap_for(p.pop) : 0;
+        m.nblk += (int)((p.pop + CHUNK - 1) / CHUNK);
+    }
+    m.lay = make_layout(m.ps);
+    m.mp_off = align_up(m.lay.total);
+    m.tie_off = align_up(m.mp_off + (size_t)n * 16);
+    m.total = align_up(m.tie_off + (size_t)(m.nblk + 1) * sizeof(uint32_t));
+    return WTP_OK;
+}
+
+size_t wtp_min_prune_workspace_size(const wtp_tensor* tensors, int ntensors, double fraction) {
+    if (ntensors < 0 || (ntensors > 0 && !tensors)) return 0;
+    MinPlan m;
+    if (plan_min(tensors, ntensors, fraction, false, m) != WTP_OK) return 0;
+    return m.total;
+}
+
+int wtp_min_prune_f32(const wtp_tensor* tensors, int ntensors, double fraction, void* ws, size_t ws_bytes,
+                      wtp_result* results, wtp_stream_t stream) {
+    g_err.clear();
+    g_err_tensor = -1;
+    if (ntensors < 0 || (ntensors > 0 && (!tensors || !results))) return fail(WTP_EARG, -1, "bad arguments");
+    if (ntensors == 0) return WTP_OK;
+    MinPlan m;
+    int rc = plan_min(tensors, ntensors, fraction, true, m);
+    if (rc != WTP_OK) return rc;
+    if (!ws || ws_bytes < m.total)
+        return fail(WTP_EWORKSPACE, -1, "workspace too small: need %zu bytes, got %zu", m.total, ws_bytes);
+    hipStream_t s = (hipStream_t)stream;
+    SelHeader* head = reinterpret_cast<SelHeader*>(wsb(ws, m.lay.sel));
+    uint32_t* cand = reinterpret_cast<uint32_t*>(wsb(ws, m.lay.cand));
+    float* thr_t = reinterpret_cast<float*>(wsb(ws, m.lay.thr));
+    void* mp = wsb(ws, m.mp_off);
+    uint32_t* tiecnt = reinterpret_cast<uint32_t*>(wsb(ws, m.tie_off));
+    /* empty tensors: nothing to select; their records are zero */
+    for (int t = 0; t < ntensors; ++t)
+        if (m.ps[t].numel == 0 && hipMemsetAsync(results + t, 0, sizeof(wtp_result), s) != hipSuccess)
+            return fail(WTP_EHIP, t, "hipMemsetAsync failed");
+    std::vector<int> live;
+    for (int t = 0; t < ntensors; ++t)
+        if (m.ps[t].numel > 0) live.push_back(t);
+    for (size_t g0 = 0; g0 < live.size(); g0 += SEG_PER_LAUNCH) {
+        SegTable tab;
+        memset(&tab, 0, sizeof tab);
+        int blk = 0;
+        for (size_t j = g0; j < live.size() && j < g0 + SEG_PER_LAUNCH; ++j) {
+            const int t = live[j];
+            const TPlan& p = m.ps[t];
+            SegDesc& sd = tab.s[tab.nseg++];
+            sd.data = tensors[t].in;
+            sd.out = tensors[t].out;
+            sd.n = p.pop;
+            sd.above = 1; /* one rank: r1 = r0 */
+            sd.gamma = 0.0;
+            sd.r0 = m.k[t] > 0 ? m.k[t] - 1 : 0;
+            sd.numel = p.numel;
+            sd.blk_begin = blk;
+            tab.blk_begin[tab.nseg - 1] = blk;
+            sd.slot = (int)(j - g0);
+            sd.res = t;
+            sd.eff_level = 0;
+            sd.flags = SEG_MINPRUNE | (m.k[t] == 0 ? SEG_KZERO : 0);
+            const uintptr_t a = reinterpret_cast<uintptr_t>(sd.data), o = reinterpret_cast<uintptr_t>(sd.out);
+            if ((a % 16) == 0 && (o % 16) == 0) sd.flags |= SEG_ALIGNED;
+            sd.cand_off = (int64_t)p.cand_off;
+            sd.cap = p.cap;
+            bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap);
+            blk += (int)((p.pop + CHUNK - 1) / CHUNK);
+        }
+        tab.nblk = blk;
+        for (int i = tab.nseg; i < SEG_PER_LAUNCH; ++i) tab.blk_begin[i] = INT32_MAX;
+        launch_window(tab, head, s);
+        launch_collect(tab, head, cand, results, s);
+        launch_minprune(tab, head, cand, results, thr_t, mp, tiecnt, s);
+    }
+    return check_launch();
+}
+
 int wtp_threshold_f32(const float* in, float* out, int64_t n, double pct, void* ws, size_t ws_bytes,
                       wtp_result* result, wtp_stream_t stream) {
     wtp_tensor t;

@@ -547,18 +547,20 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
     const float diff = fb - fa;
     const double g = sd.gamma;
     double thr = (g >= 0.5) ? (double)fb - (double)diff * (1.0 - g) : (double)fa + (double)diff * g;
-    if (mk > 0x7F800000u) thr = __longlong_as_double(0x7FF8000000000000ll); /* NaN present: np.percentile is NaN */
+    const bool minp = (sd.flags & SEG_MINPRUNE) != 0; /* rank select for min pruning: no NumPy NaN rule */
+    if (mk > 0x7F800000u && !minp) thr = __longlong_as_double(0x7FF8000000000000ll); /* NaN present: np.percentile is NaN */
     const float thr32 = (float)thr;
-    const bool nan = thr32 != thr32; /* also inf - inf inside the lerp */
+    const bool nan = !minp && thr32 != thr32; /* also inf - inf inside the lerp */
     /* level-0 segments: zeros of where(|x| < thr, 0, x) = #(key < tk) with tk = bits(thr) when
      * thr > 0, else tk = 1 (only the zeros themselves).  ka <= thr <= kb and the two ranks are
      * adjacent, so #(key < tk) = below + [tk > kl] eq_lo + before + #(staged < tk).  A NaN
      * threshold prunes nothing: every k_mask_select block counts the zeros of its copy. */
     WTP_PROBE(5);
-    if (!publish) return thr32; /* block-uniform */
+    if (!publish) return minp ? __uint_as_float(ka) : thr32; /* block-uniform */
     int64_t zc = 0;
-    if ((sd.flags & SEG_MASK) && !nan) {
-        const uint32_t tk = thr32 > 0.0f ? __float_as_uint(thr32) : 1u;
+    /* min pruning (k_minsel) wants #(key < t) for the exact key t = ka: none when t == 0 */
+    if (((sd.flags & SEG_MASK) || (minp && ka > 0)) && !nan) {
+        const uint32_t tk = minp ? ka : (thr32 > 0.0f ? __float_as_uint(thr32) : 1u);
         if (path == MODE_FULL)
             zc = block_count_below<THREADS>([&](int64_t i) { return abs_key(x[i]); }, sd.n, tk);
         else if (path == MODE_CAND)
@@ -578,7 +580,8 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
         wtp_result& r = res[sd.res];
         r.numel = sd.numel;
         r.coeff_numel = sd.n;
-        if (zc) atomicAdd((unsigned long long*)&r.zero_count, (unsigned long long)zc); /* zeroed by k_collect */
+        if (minp) r.zero_count = zc; /* k_minsel turns it into the tie budget; k_minmask counts */
+        else if (zc) atomicAdd((unsigned long long*)&r.zero_count, (unsigned long long)zc); /* zeroed by k_collect */
         r.thr64 = thr;
         r.thr32_bits = __float_as_uint(thr32);
         r.max_abs_bits = mk;
@@ -586,7 +589,7 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
         r.path = path;
     }
     WTP_PROBE(6);
-    return thr32;
+    return minp ? __uint_as_float(ka) : thr32;
 }
 
 /* k_window: one 1024-thread block per segment derives the window of the region k_collect is
@@ -760,6 +763,159 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_mask_select(SegTable t, cons
     }
 }
 
+/* -------------------------------------------------------- min-weight pruning --- */
+/* percentage_min_pruning (ResNet/min_weight_pruning.py:66-74): zero the k smallest |w| of each
+ * tensor.  The rank-(k-1) key t comes from the same window / collect / select machinery
+ * (r0 = k-1, gamma 0).  Every |w| < t is pruned; of the |w| == t the lowest flat indices go
+ * first until k are pruned (torch.topk's order among ties is unspecified).
+ *   k_minsel   one block per segment: the exact t, and need = k - #(|w| < t)
+ *   k_tiecount one block per chunk: #(|w| == t) in the chunk
+ *   k_minmask  one block per chunk: its ties' global order = the counts of the segment's
+ *              earlier chunks + an in-block scan in flat-index order; writes out, counts zeros */
+struct MinPrune {
+    uint32_t tkey;   /* |w| bit pattern of t (k = 0: 0, with need 0 nothing is pruned) */
+    uint32_t pad;
+    int64_t need;    /* ties to prune (lowest indices first) */
+};
+
+__global__ __launch_bounds__(STREAM_THREADS) void k_minsel(SegTable t, const SelHeader* __restrict__ head,
+                                                           const uint32_t* __restrict__ cand,
+                                                           wtp_result* __restrict__ res, float* __restrict__ thr_out,
+                                                           MinPrune* __restrict__ mp) {
+    __shared__ uint32_t stage[4096];
+    const SegDesc& sd = t.s[blockIdx.x];
+    const SelState* st = sel_region(const_cast<SelHeader*>(head), head->parity ^ 1u) + sd.slot;
+    const int64_t k = (sd.flags & SEG_KZERO) ? 0 : sd.r0 + 1;
+    float thr = 0.0f;
+    if (k > 0) thr = select_body<STREAM_THREADS>(sd, st, cand, res, thr_out, stage, 4096, true);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        wtp_result& r = res[sd.res];
+        MinPrune m;
+        m.pad = 0;
+        if (k > 0) {
+            m.tkey = __float_as_uint(thr) & 0x7FFFFFFFu;
+            m.need = k - r.zero_count; /* select_body left #(|w| < t) there */
+        } else { /* nothing to prune */
+            r.numel = sd.numel;
+            r.coeff_numel = sd.n;
+            r.thr64 = 0.0;
+            r.thr32_bits = 0;
+            r.max_abs_bits = 0;
+            r.eff_level = 0;
+            r.path = MODE_WINDOW;
+            m.tkey = 0; /* no key is below 0, and no tie is pruned */
+            m.need = 0;
+        }
+        r.zero_count = 0; /* k_minmask adds the zeros it writes */
+        mp[sd.res] = m;
+    }
+}
+
+__global__ __launch_bounds__(STREAM_THREADS) void k_tiecount(SegTable t, const MinPrune* __restrict__ mp,
+                                                             uint32_t* __restrict__ tiecnt) {
+    const int si = find_seg(t, blockIdx.x);
+    const SegDesc& sd = t.s[si];
+    const MinPrune m = mp[sd.res];
+    const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * CHUNK;
+    const int len = (int)min((int64_t)CHUNK, sd.n - base);
+    uint32_t c = 0;
+    if (m.need > 0) { /* block-uniform */
+        float4 v[16];
+        if ((sd.flags & SEG_ALIGNED) && len == CHUNK) load_chunk<16>(sd.data + base, v);
+        else load_chunk_ragged<16>(sd.data + base, len, v);
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int e = 4 * (it * STREAM_THREADS + (int)threadIdx.x);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c += (e + q < len) && abs_key(f4_get(v[it], q)) == m.tkey;
+        }
+    }
+    const unsigned long long tot = block_sum_u64<STREAM_THREADS>(c);
+    if (threadIdx.x == 0) tiecnt[blockIdx.x] = (uint32_t)tot;
+}
+
+__global__ __launch_bounds__(STREAM_THREADS) void k_minmask(SegTable t, const MinPrune* __restrict__ mp,
+                                                            const uint32_t* __restrict__ tiecnt,
+                                                            wtp_result* __restrict__ res) {
+    __shared__ uint32_t wsum[STREAM_THREADS / 64];
+    __shared__ int64_t s_off;
+    const int si = find_seg(t, blockIdx.x);
+    const SegDesc& sd = t.s[si];
+    const MinPrune m = mp[sd.res];
+    const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * CHUNK;
+    const int len = (int)min((int64_t)CHUNK, sd.n - base);
+    const bool full = (sd.flags & SEG_ALIGNED) && len == CHUNK;
+    float4 v[16];
+    if (full) load_chunk<16>(sd.data + base, v);
+    else load_chunk_ragged<16>(sd.data + base, len, v);
+    /* ties of the segment's earlier chunks */
+    const bool ties = m.need > 0 && tiecnt[blockIdx.x] > 0; /* block-uniform */
+    if (ties && threadIdx.x < 64) {
+        unsigned long long a = 0;
+        for (int b = sd.blk_begin + (int)threadIdx.x; b < (int)blockIdx.x; b += 64) a += tiecnt[b];
+        a = wave_sum_u64(a);
+        if (threadIdx.x == 0) s_off = (int64_t)a;
+    }
+    __syncthreads();
+    int64_t run = ties ? s_off : 0; /* ties before the current it-row */
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    unsigned long long z = 0;
+    auto prune = [&](uint32_t k, int64_t rank) { return k < m.tkey || (k == m.tkey && rank < m.need); };
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int e = 4 * (it * STREAM_THREADS + (int)threadIdx.x);
+        float4 y = v[it];
+        if (ties) { /* flat-index order inside the block: it-row, then thread, then component */
+            uint32_t c = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c += (e + q < len) && abs_key(f4_get(v[it], q)) == m.tkey;
+            const uint32_t incl = wave_scan_u32(c);
+            if (lane == 63) wsum[wv] = incl;
+            __syncthreads();
+            int64_t before = run + (incl - c);
+            uint32_t rowtot = 0;
+            for (int w = 0; w < STREAM_THREADS / 64; ++w) {
+                if (w < wv) before += wsum[w];
+                rowtot += wsum[w];
+            }
+            __syncthreads();
+            run += rowtot;
+            float* yy = reinterpret_cast<float*>(&y);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t k = abs_key(yy[q]);
+                if (prune(k, before)) yy[q] = 0.0f;
+                before += (e + q < len) && k == m.tkey;
+            }
+        } else {
+            float* yy = reinterpret_cast<float*>(&y);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (abs_key(yy[q]) < m.tkey) yy[q] = 0.0f;
+        }
+        v[it] = y;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) z += (e + q < len) && f4_get(y, q) == 0.0f;
+    }
+    float* q = sd.out + base;
+    if (full) {
+        float4* q4 = reinterpret_cast<float4*>(q);
+#pragma unroll
+        for (int it = 0; it < 16; ++it) q4[it * STREAM_THREADS + threadIdx.x] = v[it];
+    } else {
+        const __amdgpu_buffer_rsrc_t r = ragged_rsrc(q, len);
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int e = 4 * (it * STREAM_THREADS + (int)threadIdx.x);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f4_get(v[it], c)), r, 4 * (e + c), 0, 0);
+        }
+    }
+    const unsigned long long tot = block_sum_u64<STREAM_THREADS>(z);
+    if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long*)&res[sd.res].zero_count, tot);
+}
+
 /* ------------------------------------------------------------ filter bank --- */
 constexpr int DWT_THREADS = 256;
 
@@ -899,6 +1055,15 @@ void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_resu
     hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT, COLLECT_WINDOW_INLINE>),
                        dim3(t.nblk * (CHUNK / (COLLECT_IT * COLLECT_THREADS * 4))), dim3(COLLECT_THREADS), 0, s, t,
                        head, cand, res);
+}
+void launch_minprune(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
+                     void* mp, uint32_t* tiecnt, hipStream_t s) {
+    hipLaunchKernelGGL(k_minsel, dim3(t.nseg), dim3(STREAM_THREADS), 0, s, t, head, cand, res, thr_out,
+                       reinterpret_cast<MinPrune*>(mp));
+    hipLaunchKernelGGL(k_tiecount, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, reinterpret_cast<const MinPrune*>(mp),
+                       tiecnt);
+    hipLaunchKernelGGL(k_minmask, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, reinterpret_cast<const MinPrune*>(mp),
+                       tiecnt, res);
 }
 void launch_mask_select(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
                         hipStream_t s) {

@@ -60,6 +60,8 @@ constexpr int SEG_PER_LAUNCH = 24;
 enum SegFlags : int32_t {
     SEG_MASK = 1,      /* level-0 / 1-D: the mask pass writes `out` from `data`   */
     SEG_ALIGNED = 2,   /* data (and out) 16-byte aligned: float4 path              */
+    SEG_MINPRUNE = 4,  /* min-weight pruning: rank k-1 = r0 select, k_minmask writes */
+    SEG_KZERO = 8,     /* min-weight pruning with k = 0: nothing pruned              */
 };
 
 struct SegDesc {
@@ -143,6 +145,10 @@ void launch_window(const SegTable& t, SelHeader* head, hipStream_t s);
 void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s);
 void launch_mask_select(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
                         hipStream_t s);
+/* min-weight pruning after window + collect: mp = 16 B per tensor, tiecnt = one u32 per
+ * streaming block */
+void launch_minprune(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
+                     void* mp, uint32_t* tiecnt, hipStream_t s);
 
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
                      hipStream_t s);

@@ -139,6 +139,35 @@ def prune(tensors, wavelet, level, pct, outs=None, carry_level=True):
     return outs, decode(res, len(tensors))
 
 
+def min_prune(tensors, fraction, outs=None):
+    """percentage_min_pruning (min_weight_pruning.py:66-74) of every tensor (CUDA float32) in one
+    launch sequence: zero the int(numel * fraction) smallest |w|; ties at the boundary lowest
+    flat index first.  Returns (outs, records); outs may be the inputs (in place)."""
+    check_tensors(tensors)
+    tensors = [x.contiguous() for x in tensors]
+    if outs is None:
+        outs = [torch.empty_like(x) for x in tensors]
+    n = len(tensors)
+    if n == 0:
+        return outs, []
+    device = tensors[0].device
+    L = N.lib()
+    desc = _as_desc(tensors, outs)
+    nbytes = L.wtp_min_prune_workspace_size(desc, n, float(fraction))
+    ws = workspace(device, nbytes if nbytes else 256)
+    res = torch.empty(n * N.RESULT_BYTES, dtype=torch.uint8, device=device)
+    rc = L.wtp_min_prune_f32(desc, n, float(fraction), ws.data_ptr(), ws.numel(), res.data_ptr(),
+                             ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream))
+    if rc != N.WTP_OK:
+        msg = N.last_error()
+        if rc == N.WTP_EARG and "NaN" in msg:
+            raise ValueError(msg)
+        if rc == N.WTP_EARG:
+            raise RuntimeError(msg)  # torch.topk: "selected index k out of range"
+        raise_for(rc, tensors, None)
+    return outs, decode(res, n)
+
+
 def threshold(x, pct, out=None):
     """percentile_based_thresholding (dwt_pruning.py:25-32) of a CUDA float32 tensor."""
     check_tensors([x])
