@@ -1,0 +1,73 @@
+"""End-to-end caller run: what main_pruning.py does with this path --
+a Hugging Face ResNet-18 (the reference's model family and layer names, random init: the
+pretrained weights are not available offline) through wavelet_pruning (selective log, saved
+model, experiment log) and then the min-weight baseline -- on the GPU, checked layer by layer
+against the CPU oracle and against the count rules the reference's stored logs follow."""
+import copy
+import csv
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _resnet18():
+    from transformers import ResNetConfig, ResNetForImageClassification
+    torch.manual_seed(0)
+    cfg = ResNetConfig(embedding_size=64, hidden_sizes=[64, 128, 256, 512], depths=[2, 2, 2, 2], layer_type="basic")
+    return ResNetForImageClassification(cfg).eval()
+
+
+def test_main_pruning_sequence(tmp_path, capsys):
+    assert torch.cuda.is_available()
+    from wavelettransforms_amd.dwt_pruning import wavelet_pruning
+    from wavelettransforms_amd.min_weight_pruning import min_weight_pruning
+    model = _resnet18()
+    min_model = copy.deepcopy(model)
+    convs = [(n, m) for n, m in model.named_modules() if isinstance(m, torch.nn.Conv2d)]
+    before = {n: m.weight.detach().cpu().numpy().copy() for n, m in convs}
+    work = tmp_path / "a" / "b"  # outputs go to <cwd>/../../WaveletTransforms/ResNet/SavedModels
+    work.mkdir(parents=True)
+    cwd = os.getcwd()
+    os.chdir(work)
+    try:
+        exp_csv = str(tmp_path / "experiment_log.csv")
+        log_path = wavelet_pruning(model, "bior4.4", 5, 0.382 * 100, exp_csv, "e2e0guid")   # main_pruning.py:185
+        min_weight_pruning(min_model, log_path, "e2e0guid", "bior4.4", 5, 0.382, exp_csv)    # :200-208
+    finally:
+        os.chdir(cwd)
+    out = capsys.readouterr().out
+    root = tmp_path / "WaveletTransforms" / "ResNet" / "SavedModels" / "bior4.4_threshold-0.382_level-5_guid-e2e0"
+    assert os.path.samefile(log_path, root / "selective_pruned" / "log.csv")
+    rows = list(csv.DictReader(open(log_path)))
+    assert [r["Layer Name"] for r in rows] == [n for n, _ in convs]
+    total = 0
+    for (name, m), r in zip(convs, rows):
+        ref, rr = O.prune_tensor(before[name], "bior4.4", 5, 0.382 * 100)
+        assert np.array_equal(m.weight.detach().cpu().numpy(), ref), name      # weights bit for bit
+        n = int(r["Original Parameter Count"])
+        assert n == ref.size and int(r["Total Pruned Count"]) == rr["zero_count"]
+        assert int(r["Non-zero Params"]) == n - rr["zero_count"]
+        # the stored logs' rule for level-0 layers without ties: floor((n-1)q) + 1 pruned, or one
+        # fewer when the f32 threshold rounds onto s[floor((n-1)q)] (4 such rows in the logs)
+        assert rr["zero_count"] - (math.floor((n - 1) * 0.382) + 1) in (0, -1), name
+        total += rr["zero_count"]
+    assert (root / "selective_pruned" / "model.safetensors").exists()
+    assert (root / "selective_pruned" / "config.json").exists()
+    exp = list(csv.reader(open(exp_csv)))
+    assert exp[1][4] == "selective" and int(exp[1][5]) == total
+    # the min-weight baseline: pruned = int(n * p), p = the DWT run's overall fraction
+    p = total / sum(int(r["Original Parameter Count"]) for r in rows)
+    mins = list(csv.DictReader(open(root / "min_pruned" / "log.csv")))
+    assert [r["Layer Name"] for r in mins] == [n for n, _ in convs]
+    for r, (name, m) in zip(mins, [(n, m) for n, m in min_model.named_modules() if isinstance(m, torch.nn.Conv2d)]):
+        n = int(r["Original Parameter Count"])
+        assert int(r["Total Pruned Count"]) == int(n * p) == int((m.weight == 0).sum()), name
+    assert exp[2][4] == "min"
+    assert "Selectively pruned model saved at" in out and "Minimum weight pruning completed." in out
