@@ -111,6 +111,30 @@ def test_batched_resnet18_equals_oracle_per_layer(eng):
         assert r["zero_count"] == rr["zero_count"] and G.f64_bits_equal(r["thr64"], rr["thr64"])
 
 
+# odd 2-D shapes raise IndexError in the reference (the crop of dwt_pruning.py:79-82 is 4-D),
+# so odd extents come with batch dims here
+MIXED_SHAPES = [(64, 64), (3, 2, 40, 70), (1, 1, 97, 130), (2, 1, 33, 33), (2, 200), (128, 784), (10, 128),
+                (5, 3, 7, 7), (64, 64, 3, 3), (256, 256), (1, 2, 77, 512), (2, 3, 31, 64), (1, 1, 513, 65),
+                (64, 32), (300, 300)]
+
+
+@pytest.mark.parametrize("wavelet", ["haar", "db8", "bior3.3", "coif2", "rbio2.2"])
+def test_grouped_levels_mixed_batch(eng, wavelet):
+    """One call over 15 tensors of mixed sizes, batch dims and clamped levels: the same level of
+    every tensor runs as one grouped filter-bank launch (more than FB_GROUP images, so the group
+    splits), small levels on the per-point kernels; each tensor == the oracle bit for bit."""
+    xs, refs = [], []
+    for j, shp in enumerate(MIXED_SHAPES):
+        e = G.W.sigma_exponent((2.0 / (shp[-1] * shp[-2])) ** 0.5)
+        xs.append(eng.synth(shp, 11, j, e))
+        refs.append(O.prune_tensor(G.W.synth_numpy(shp, 11, j, e), wavelet, 5, 37.5))
+    outs, res = eng.prune(xs, wavelet, 5, 37.5, carry_level=False)
+    for shp, o, r, (ref, rr) in zip(MIXED_SHAPES, outs, res, refs):
+        assert np.array_equal(o.cpu().numpy(), ref), shp
+        assert r["zero_count"] == rr["zero_count"] and r["eff_level"] == rr["eff_level"], shp
+        assert G.f64_bits_equal(r["thr64"], rr["thr64"]), shp
+
+
 def test_window_miss_falls_back_to_full_scan(eng):
     """Data whose sampled positions are unrepresentative: the sample window misses the true
     order statistics and k_select must fall back to the exact full radix select (path 3)."""

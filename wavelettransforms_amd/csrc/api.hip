@@ -77,11 +77,12 @@ struct TPlan {
     int64_t cap = 0;      /* candidate capacity                                         */
     size_t p_off = 0;     /* workspace byte offset of the packed array (dwt only)       */
     size_t cand_off = 0;  /* element offset into the candidate region                   */
+    size_t t_off = 0;     /* workspace byte offset of this tensor's three level temps      */
+    size_t t_elems = 0;   /* elements per temp                                              */
 };
 
 struct Layout {
-    size_t hist = 0, sel = 0, thr = 0, cand = 0, P = 0, tmp[3] = {0, 0, 0}, total = 0;
-    size_t tmp_elems = 0;
+    size_t hist = 0, sel = 0, thr = 0, cand = 0, P = 0, total = 0;
 };
 
 /* persistent slot region: identical position and size in every layout */
@@ -181,20 +182,21 @@ Layout make_layout(std::vector<TPlan>& ps) {
     for (auto& p : ps) { p.cand_off = ce; ce += (size_t)p.cap; }
     off = align_up(off + ce * sizeof(uint32_t));
     L.P = off;
-    size_t tmp = 0;
     for (auto& p : ps) {
         if (!p.dwt) continue;
         p.p_off = off;
         off = align_up(off + (size_t)p.pop * sizeof(float));
+    }
+    /* every tensor has its own level temps: the same level of all tensors runs as one grouped
+     * launch, so their intermediate approximations are live together */
+    for (auto& p : ps) {
+        if (!p.dwt) continue;
         const int64_t r1 = p.g.R[1], c1 = p.g.C[1];
         const size_t a = (size_t)(p.B * r1 * (p.W > 2 * c1 ? p.W : 2 * c1));
         const size_t b = (size_t)(p.B * 2 * r1 * 2 * c1);
-        tmp = std::max(tmp, std::max(a, b));
-    }
-    L.tmp_elems = tmp;
-    for (int i = 0; i < 3; ++i) {
-        L.tmp[i] = off;
-        off = align_up(off + tmp * sizeof(float));
+        p.t_elems = std::max(a, b);
+        p.t_off = off;
+        off = align_up(off + 3 * align_up(p.t_elems * sizeof(float)));
     }
     L.total = off;
     return L;
@@ -225,57 +227,90 @@ int check_launch() {
     return WTP_OK;
 }
 
-/* forward multi-level transform of one image batch into the packed array P */
-/* pywt.wavedec2 (dwt_pruning.py:67-68) into the packed layout: one tiled launch per level
- * (filterbank.hip) where the level is large enough, else the two per-point passes.  The
- * approximation ping-pongs between workspace temps so no launch reads what it writes. */
-void forward(const float* in, const TPlan& p, const Taps& tp, float* P, float* tL, float* tH, float* tA,
-             hipStream_t s) {
-    const float* cur = in;
-    for (int k = 1; k <= p.L; ++k) {
-        const int64_t R0 = p.g.R[k - 1], C0 = p.g.C[k - 1];
-        if (fb_tiled_ok(p.B, R0, C0, tp)) {
-            float* an = (cur == tA) ? tL : tA;
-            launch_fwd_level(cur, p.B, R0, C0, tp, an, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k], k == p.L, s);
-            cur = an;
-        } else {
-            float* t0 = (cur == tL) ? tA : tL;
-            float* t1 = (cur == tH) ? tA : tH;
-            float* an = (cur == tL || cur == tH || cur == tA) ? const_cast<float*>(cur) : tA;
-            launch_dwt_cols(cur, p.B, R0, C0, tp, t0, t1, s);
-            launch_dwt_rows(t0, t1, p.B, p.g.R[k], C0, tp, an, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k],
-                            k == p.L, s);
-            cur = an;
+/* one image batch's transform chain: its input / output, packed array and three level temps */
+struct Chain {
+    const TPlan* p;
+    const float* in;   /* forward input */
+    float* out;        /* inverse output */
+    float* P;
+    float* T[3];
+    const float* thr;
+    unsigned long long* zc;
+};
+
+/* pywt.wavedec2 (dwt_pruning.py:67-68) of every chain into its packed layout.  Level k of all
+ * chains is ONE tiled launch (filterbank.hip) where the level is large enough, else the two
+ * per-point passes of that chain.  Each approximation ping-pongs between the chain's own temps
+ * so no launch reads what it writes. */
+void forward_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s) {
+    int maxL = 0;
+    for (const Chain& c : cs) maxL = std::max(maxL, c.p->L);
+    std::vector<const float*> cur(cs.size());
+    for (size_t j = 0; j < cs.size(); ++j) cur[j] = cs[j].in;
+    std::vector<FwdItem> items;
+    for (int k = 1; k <= maxL; ++k) {
+        items.clear();
+        for (size_t j = 0; j < cs.size(); ++j) {
+            const TPlan& p = *cs[j].p;
+            if (p.L < k) continue;
+            float *tL = cs[j].T[0], *tH = cs[j].T[1], *tA = cs[j].T[2];
+            const int64_t R0 = p.g.R[k - 1], C0 = p.g.C[k - 1];
+            if (fb_tiled_ok(p.B, R0, C0, tp)) {
+                float* an = (cur[j] == tA) ? tL : tA;
+                items.push_back(FwdItem{cur[j], p.B, R0, C0, an, cs[j].P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k],
+                                        k == p.L});
+                cur[j] = an;
+            } else {
+                float* t0 = (cur[j] == tL) ? tA : tL;
+                float* t1 = (cur[j] == tH) ? tA : tH;
+                float* an = (cur[j] == tL || cur[j] == tH || cur[j] == tA) ? const_cast<float*>(cur[j]) : tA;
+                launch_dwt_cols(cur[j], p.B, R0, C0, tp, t0, t1, s);
+                launch_dwt_rows(t0, t1, p.B, p.g.R[k], C0, tp, an, cs[j].P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k],
+                                k == p.L, s);
+                cur[j] = an;
+            }
         }
+        if (!items.empty()) launch_fwd_levels(items.data(), (int)items.size(), tp, s);
     }
 }
-/* pywt.waverec2 (dwt_pruning.py:75-77) from the packed layout, thresholding the packed
- * coefficients as they are loaded (the np.where of :31), cropping and counting zeros on the
- * last level (:79-88).  Same buffer discipline as forward(). */
-void inverse(const float* P, const TPlan& p, const Taps& tp, const float* thr, float* out, unsigned long long* zc,
-             float* tL, float* tH, float* tA, hipStream_t s) {
-    const float* cur = nullptr; /* approximation of the level above (nullptr: the packed cA) */
-    for (int k = p.L; k >= 1; --k) {
-        const int64_t R = p.g.R[k], C = p.g.C[k];
-        const bool fromP = k == p.L;
-        const int64_t a_bs = fromP ? 0 : 4 * p.g.R[k + 1] * p.g.C[k + 1];
-        const int64_t lda = fromP ? 0 : 2 * p.g.C[k + 1];
-        const bool final = k == 1;
-        const int64_t oH = final ? p.H : 2 * R, oW = final ? p.W : 2 * C;
-        if (fb_tiled_ok(p.B, 2 * R, 2 * C, tp)) {
-            float* y = final ? out : ((cur == tA) ? tL : tA);
-            launch_inv_level(cur, a_bs, lda, fromP, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k], p.B, R, C, tp, thr, y,
-                             oH, oW, final ? zc : nullptr, s);
-            cur = y;
-        } else {
-            float* t0 = (cur == tL) ? tA : tL;
-            float* t1 = (cur == tH) ? tA : tH;
-            launch_idwt_rows(cur, a_bs, lda, fromP, P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k], p.B, R, C, tp, thr,
-                             t0, t1, s);
-            float* y = final ? out : (cur ? const_cast<float*>(cur) : tA);
-            launch_idwt_cols(t0, t1, p.B, R, C, tp, y, oH, oW, final ? zc : nullptr, s);
-            cur = y;
+
+/* pywt.waverec2 (dwt_pruning.py:75-77) of every chain from its packed layout, thresholding the
+ * packed coefficients as they are loaded (the np.where of :31), cropping and counting zeros on
+ * the last level (:79-88).  Level k of all chains is one launch, as in forward_chains(). */
+void inverse_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s) {
+    int maxL = 0;
+    for (const Chain& c : cs) maxL = std::max(maxL, c.p->L);
+    std::vector<const float*> cur(cs.size(), nullptr); /* nullptr: the packed cA */
+    std::vector<InvItem> items;
+    for (int k = maxL; k >= 1; --k) {
+        items.clear();
+        for (size_t j = 0; j < cs.size(); ++j) {
+            const TPlan& p = *cs[j].p;
+            if (p.L < k) continue;
+            float *tL = cs[j].T[0], *tH = cs[j].T[1], *tA = cs[j].T[2];
+            const int64_t R = p.g.R[k], C = p.g.C[k];
+            const bool fromP = k == p.L;
+            const int64_t a_bs = fromP ? 0 : 4 * p.g.R[k + 1] * p.g.C[k + 1];
+            const int64_t lda = fromP ? 0 : 2 * p.g.C[k + 1];
+            const bool final = k == 1;
+            const int64_t oH = final ? p.H : 2 * R, oW = final ? p.W : 2 * C;
+            unsigned long long* zc = final ? cs[j].zc : nullptr;
+            if (fb_tiled_ok(p.B, 2 * R, 2 * C, tp)) {
+                float* y = final ? cs[j].out : ((cur[j] == tA) ? tL : tA);
+                items.push_back(InvItem{cur[j], a_bs, lda, fromP, cs[j].P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k],
+                                        p.B, R, C, cs[j].thr, y, oH, oW, zc});
+                cur[j] = y;
+            } else {
+                float* t0 = (cur[j] == tL) ? tA : tL;
+                float* t1 = (cur[j] == tH) ? tA : tH;
+                launch_idwt_rows(cur[j], a_bs, lda, fromP, cs[j].P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k], p.B, R,
+                                 C, tp, cs[j].thr, t0, t1, s);
+                float* y = final ? cs[j].out : (cur[j] ? const_cast<float*>(cur[j]) : tA);
+                launch_idwt_cols(t0, t1, p.B, R, C, tp, y, oH, oW, zc, s);
+                cur[j] = y;
+            }
         }
+        if (!items.empty()) launch_inv_levels(items.data(), (int)items.size(), tp, s);
     }
 }
 
@@ -343,21 +378,28 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     SelHeader* head = reinterpret_cast<SelHeader*>(wsb(ws, lay.sel));
     uint32_t* cand = reinterpret_cast<uint32_t*>(wsb(ws, lay.cand));
     float* thr_t = reinterpret_cast<float*>(wsb(ws, lay.thr));
-    float* tL = reinterpret_cast<float*>(wsb(ws, lay.tmp[0]));
-    float* tH = reinterpret_cast<float*>(wsb(ws, lay.tmp[1]));
-    float* tA = reinterpret_cast<float*>(wsb(ws, lay.tmp[2]));
     const Taps tp = (wavelet_id >= 0 && wavelet_id < WT_NUM_WAVELETS) ? make_taps(wavelet_id) : Taps{};
 
     stage(0, s);
     /* 1. forward transforms into the packed arrays (pywt.wavedec2 + coeffs_to_array) */
+    std::vector<Chain> chains;
     for (int t = 0; t < ntensors; ++t) {
         const TPlan& p = ps[t];
         if (!p.dwt) continue;
-        float* P = reinterpret_cast<float*>(wsb(ws, p.p_off));
-        if (!p.tight && hipMemsetAsync(P, 0, (size_t)p.pop * sizeof(float), s) != hipSuccess)
+        Chain c;
+        c.p = &p;
+        c.in = tensors[t].in;
+        c.out = tensors[t].out;
+        c.P = reinterpret_cast<float*>(wsb(ws, p.p_off));
+        for (int i = 0; i < 3; ++i)
+            c.T[i] = reinterpret_cast<float*>(wsb(ws, p.t_off + i * align_up(p.t_elems * sizeof(float))));
+        c.thr = thr_t + t;
+        c.zc = reinterpret_cast<unsigned long long*>(&results[t].zero_count);
+        chains.push_back(c);
+        if (!p.tight && hipMemsetAsync(c.P, 0, (size_t)p.pop * sizeof(float), s) != hipSuccess)
             return fail(WTP_EHIP, t, "hipMemsetAsync failed");
-        forward(tensors[t].in, p, tp, P, tL, tH, tA, s);
     }
+    forward_chains(chains, tp, s);
     /* 2. exact percentile selection + level-0 mask, SEG_PER_LAUNCH segments per launch group */
     for (int g0 = 0; g0 < ntensors; g0 += SEG_PER_LAUNCH) {
         SegTable tab;
@@ -396,13 +438,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         if (first) stage(4, s);
     }
     /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2) */
-    for (int t = 0; t < ntensors; ++t) {
-        const TPlan& p = ps[t];
-        if (!p.dwt) continue;
-        const float* P = reinterpret_cast<const float*>(wsb(ws, p.p_off));
-        inverse(P, p, tp, thr_t + t, tensors[t].out,
-                reinterpret_cast<unsigned long long*>(&results[t].zero_count), tL, tH, tA, s);
-    }
+    inverse_chains(chains, tp, s);
     stage(5, s);
     return check_launch();
 }
@@ -583,7 +619,7 @@ int wtp_wavedec2_f32(const float* in, float* packed, int64_t B, int64_t H, int64
     float* tA = reinterpret_cast<float*>(wsb(ws, 2 * one));
     if (!p.tight && hipMemsetAsync(packed, 0, (size_t)p.pop * sizeof(float), s) != hipSuccess)
         return fail(WTP_EHIP, -1, "hipMemsetAsync failed");
-    forward(in, p, make_taps(wid), packed, tL, tH, tA, s);
+    forward_chains({Chain{&p, in, nullptr, packed, {tL, tH, tA}, nullptr, nullptr}}, make_taps(wid), s);
     return check_launch();
 }
 
@@ -603,7 +639,7 @@ int wtp_waverec2_f32(const float* packed, float* out, int64_t B, int64_t H, int6
     float* tL = reinterpret_cast<float*>(wsb(ws, 0));
     float* tH = reinterpret_cast<float*>(wsb(ws, one));
     float* tA = reinterpret_cast<float*>(wsb(ws, 2 * one));
-    inverse(packed, p, make_taps(wid), thr32, out, nullptr, tL, tH, tA, s);
+    inverse_chains({Chain{&p, nullptr, out, const_cast<float*>(packed), {tL, tH, tA}, thr32, nullptr}}, make_taps(wid), s);
     return check_launch();
 }
 

@@ -20,6 +20,8 @@
 #include "wtp_internal.h"
 #include "wt_dwt_core.h"
 
+#include <cstring>
+
 #pragma clang fp contract(off)
 
 namespace wtp {
@@ -44,6 +46,13 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
     const int per = (n + 7) / 8, x = b & 7, k = b >> 3;
     const int full = n - 8 * (per - 1); /* XCDs that get `per` tiles; the rest get per - 1 */
     return x < full ? x * per + k : full * per + (x - full) * (per - 1) + k;
+}
+
+__device__ __forceinline__ int find_item(const int* blk_begin, int b) {
+    int i = 0; /* blk_begin[0] == 0 */
+#pragma unroll
+    for (int j = 1; j < FB_GROUP; ++j) i += b >= blk_begin[j];
+    return i;
 }
 
 __device__ __forceinline__ int ext_idx(int t, int N) { /* wt_ext_index in 32 bits */
@@ -247,8 +256,15 @@ struct FwdArgs {
     int last, tilesC, tilesR;
 };
 
+/* one launch covers the same level of up to FB_GROUP images (same filter): a block finds its
+ * image by one scalar sweep of blk_begin, as k_collect finds its segment */
+struct FwdGroup {
+    int blk_begin[FB_GROUP]; /* INT32_MAX past n */
+    FwdArgs it[FB_GROUP];
+};
+
 template <int FT>
-__global__ __launch_bounds__(FB_THREADS) void k_fwd_level(FwdArgs a, Taps tp) {
+__global__ __launch_bounds__(FB_THREADS) void k_fwd_level(FwdGroup g, Taps tp) {
     extern __shared__ float lds[];
     const int F = FT ? FT : tp.F;
     const int NR = 2 * FR + F - 2, NC = 2 * FC + F - 2;
@@ -258,7 +274,10 @@ __global__ __launch_bounds__(FB_THREADS) void k_fwd_level(FwdArgs a, Taps tp) {
                                                               at stride 2 stay conflict-free) */
     const int HALF = (NC + 1) / 2;
     auto lhi = [&](int o, int cc) { return o * NC + (cc & 1) * HALF + (cc >> 1); };
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int gt = xcd_tile(blockIdx.x, gridDim.x);
+    const int item = find_item(g.blk_begin, gt);
+    const auto& a = g.it[item];
+    const int tile = gt - g.blk_begin[item];
     const int tc = tile % a.tilesC, tr = (tile / a.tilesC) % a.tilesR, b = tile / (a.tilesC * a.tilesR);
     const int o0r = tr * FR, o0c = tc * FC;
     const int gr0 = 2 * o0r - F / 2 + 1, gc0 = 2 * o0c - F / 2 + 1;
@@ -380,12 +399,20 @@ struct InvArgs {
     int tilesC, tilesR;
 };
 
+struct InvGroup {
+    int blk_begin[FB_GROUP];
+    InvArgs it[FB_GROUP];
+};
+
 template <int FT>
-__global__ __launch_bounds__(FB_THREADS) void k_inv_level(InvArgs a, Taps tp) {
+__global__ __launch_bounds__(FB_THREADS) void k_inv_level(InvGroup g, Taps tp) {
     extern __shared__ float lds[];
     const int F = FT ? FT : tp.F;
     const int H = F / 2;
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int gt = xcd_tile(blockIdx.x, gridDim.x);
+    const int item = find_item(g.blk_begin, gt);
+    const auto& a = g.it[item];
+    const int tile = gt - g.blk_begin[item];
     const int tc = tile % a.tilesC, tr = (tile / a.tilesC) % a.tilesR, b = tile / (a.tilesC * a.tilesR);
     const int n0 = tr * IR, m0 = tc * IC;
     const int nl = min(n0 + IR, a.outH) - 1, ml = min(m0 + IC, a.outW) - 1;
@@ -532,14 +559,12 @@ static size_t inv_lds(int F) {
 }
 
 template <int FT>
-static void fwd_go(const FwdArgs& a, int B, const Taps& tp, hipStream_t s) {
-    const int grid = a.tilesC * a.tilesR * B;
-    hipLaunchKernelGGL(k_fwd_level<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F), s, a, tp);
+static void fwd_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
+    hipLaunchKernelGGL(k_fwd_level<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F), s, g, tp);
 }
 template <int FT>
-static void inv_go(const InvArgs& a, int B, const Taps& tp, hipStream_t s) {
-    const int grid = a.tilesC * a.tilesR * B;
-    hipLaunchKernelGGL(k_inv_level<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F), s, a, tp);
+static void inv_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
+    hipLaunchKernelGGL(k_inv_level<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F), s, g, tp);
 }
 
 /* The tiled path needs an even filter, the LDS budget, and images large enough that a tile
@@ -550,71 +575,123 @@ bool fb_tiled_ok(int64_t B, int64_t R, int64_t C, const Taps& tp) {
     return R * C >= 512; /* at least a quarter of a forward tile of outputs */
 }
 
-void launch_fwd_level(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* anext, float* P,
-                      int64_t PR, int64_t PC, int64_t offR, int64_t offC, int last, hipStream_t s) {
+static FwdArgs fwd_args(const FwdItem& x) {
     FwdArgs a;
-    a.in = in;
-    a.in_bs = R * C;
-    a.R = (int)R;
-    a.C = (int)C;
-    a.Ro = (int)((R + 1) / 2);
-    a.Co = (int)((C + 1) / 2);
-    a.P = P;
-    a.P_bs = PR * PC;
-    a.PC = (int)PC;
-    a.offR = (int)offR;
-    a.offC = (int)offC;
-    a.anext = anext;
-    a.last = last;
+    a.in = x.in;
+    a.in_bs = x.R * x.C;
+    a.R = (int)x.R;
+    a.C = (int)x.C;
+    a.Ro = (int)((x.R + 1) / 2);
+    a.Co = (int)((x.C + 1) / 2);
+    a.P = x.P;
+    a.P_bs = x.PR * x.PC;
+    a.PC = (int)x.PC;
+    a.offR = (int)x.offR;
+    a.offC = (int)x.offC;
+    a.anext = x.anext;
+    a.last = x.last;
     a.tilesC = (a.Co + FC - 1) / FC;
     a.tilesR = (a.Ro + FR - 1) / FR;
-    switch (tp.F) {
-    case 2: fwd_go<2>(a, (int)B, tp, s); break;
-    case 4: fwd_go<4>(a, (int)B, tp, s); break;
-    case 6: fwd_go<6>(a, (int)B, tp, s); break;
-    case 8: fwd_go<8>(a, (int)B, tp, s); break;
-    case 10: fwd_go<10>(a, (int)B, tp, s); break;
-    case 12: fwd_go<12>(a, (int)B, tp, s); break;
-    case 16: fwd_go<16>(a, (int)B, tp, s); break;
-    case 18: fwd_go<18>(a, (int)B, tp, s); break;
-    default: fwd_go<0>(a, (int)B, tp, s); break;
+    return a;
+}
+
+static InvArgs inv_args(const InvItem& x) {
+    InvArgs a;
+    a.a = x.a_src ? x.a_src : x.P;
+    a.a_bs = x.a_bs;
+    a.lda = (int)x.lda;
+    a.a_from_P = x.a_from_P;
+    a.P = x.P;
+    a.P_bs = x.PR * x.PC;
+    a.PC = (int)x.PC;
+    a.offR = (int)x.offR;
+    a.offC = (int)x.offC;
+    a.R = (int)x.R;
+    a.C = (int)x.C;
+    a.y = x.y;
+    a.outH = (int)x.outH;
+    a.outW = (int)x.outW;
+    a.thr = x.thr;
+    a.zc = x.zc;
+    a.tilesC = (int)((x.outW + IC - 1) / IC);
+    a.tilesR = (int)((x.outH + IR - 1) / IR);
+    return a;
+}
+
+/* Each launch takes up to FB_GROUP items whose tile counts sum below 2^31 (fb_tiled_ok bounds
+ * every item's B * R * C below 2^31 elements, hence its tiles far below). */
+void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) {
+    for (int i0 = 0; i0 < n;) {
+        FwdGroup g;
+        memset(&g, 0, sizeof g);
+        int64_t blk = 0;
+        int m = 0;
+        for (; m < FB_GROUP && i0 + m < n; ++m) {
+            g.it[m] = fwd_args(it[i0 + m]);
+            const int64_t tiles = (int64_t)g.it[m].tilesC * g.it[m].tilesR * it[i0 + m].B;
+            if (m > 0 && blk + tiles > INT32_MAX) break;
+            g.blk_begin[m] = (int)blk;
+            blk += tiles;
+        }
+        for (int j = m; j < FB_GROUP; ++j) g.blk_begin[j] = INT32_MAX;
+        const int grid = (int)blk;
+        switch (tp.F) {
+        case 2: fwd_go<2>(g, grid, tp, s); break;
+        case 4: fwd_go<4>(g, grid, tp, s); break;
+        case 6: fwd_go<6>(g, grid, tp, s); break;
+        case 8: fwd_go<8>(g, grid, tp, s); break;
+        case 10: fwd_go<10>(g, grid, tp, s); break;
+        case 12: fwd_go<12>(g, grid, tp, s); break;
+        case 16: fwd_go<16>(g, grid, tp, s); break;
+        case 18: fwd_go<18>(g, grid, tp, s); break;
+        default: fwd_go<0>(g, grid, tp, s); break;
+        }
+        i0 += m;
     }
+}
+
+void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s) {
+    for (int i0 = 0; i0 < n;) {
+        InvGroup g;
+        memset(&g, 0, sizeof g);
+        int64_t blk = 0;
+        int m = 0;
+        for (; m < FB_GROUP && i0 + m < n; ++m) {
+            g.it[m] = inv_args(it[i0 + m]);
+            const int64_t tiles = (int64_t)g.it[m].tilesC * g.it[m].tilesR * it[i0 + m].B;
+            if (m > 0 && blk + tiles > INT32_MAX) break;
+            g.blk_begin[m] = (int)blk;
+            blk += tiles;
+        }
+        for (int j = m; j < FB_GROUP; ++j) g.blk_begin[j] = INT32_MAX;
+        const int grid = (int)blk;
+        switch (tp.F) {
+        case 2: inv_go<2>(g, grid, tp, s); break;
+        case 4: inv_go<4>(g, grid, tp, s); break;
+        case 6: inv_go<6>(g, grid, tp, s); break;
+        case 8: inv_go<8>(g, grid, tp, s); break;
+        case 10: inv_go<10>(g, grid, tp, s); break;
+        case 12: inv_go<12>(g, grid, tp, s); break;
+        case 16: inv_go<16>(g, grid, tp, s); break;
+        case 18: inv_go<18>(g, grid, tp, s); break;
+        default: inv_go<0>(g, grid, tp, s); break;
+        }
+        i0 += m;
+    }
+}
+
+void launch_fwd_level(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* anext, float* P,
+                      int64_t PR, int64_t PC, int64_t offR, int64_t offC, int last, hipStream_t s) {
+    const FwdItem x{in, B, R, C, anext, P, PR, PC, offR, offC, last};
+    launch_fwd_levels(&x, 1, tp, s);
 }
 
 void launch_inv_level(const float* a_src, int64_t a_bs, int64_t lda, int a_from_P, const float* P, int64_t PR,
                       int64_t PC, int64_t offR, int64_t offC, int64_t B, int64_t R, int64_t C, const Taps& tp,
                       const float* thr, float* y, int64_t outH, int64_t outW, unsigned long long* zc,
                       hipStream_t s) {
-    InvArgs a;
-    a.a = a_src ? a_src : P;
-    a.a_bs = a_bs;
-    a.lda = (int)lda;
-    a.a_from_P = a_from_P;
-    a.P = P;
-    a.P_bs = PR * PC;
-    a.PC = (int)PC;
-    a.offR = (int)offR;
-    a.offC = (int)offC;
-    a.R = (int)R;
-    a.C = (int)C;
-    a.y = y;
-    a.outH = (int)outH;
-    a.outW = (int)outW;
-    a.thr = thr;
-    a.zc = zc;
-    a.tilesC = (int)((outW + IC - 1) / IC);
-    a.tilesR = (int)((outH + IR - 1) / IR);
-    switch (tp.F) {
-    case 2: inv_go<2>(a, (int)B, tp, s); break;
-    case 4: inv_go<4>(a, (int)B, tp, s); break;
-    case 6: inv_go<6>(a, (int)B, tp, s); break;
-    case 8: inv_go<8>(a, (int)B, tp, s); break;
-    case 10: inv_go<10>(a, (int)B, tp, s); break;
-    case 12: inv_go<12>(a, (int)B, tp, s); break;
-    case 16: inv_go<16>(a, (int)B, tp, s); break;
-    case 18: inv_go<18>(a, (int)B, tp, s); break;
-    default: inv_go<0>(a, (int)B, tp, s); break;
-    }
+    const InvItem x{a_src, a_bs, lda, a_from_P, P, PR, PC, offR, offC, B, R, C, thr, y, outH, outW, zc};
+    launch_inv_levels(&x, 1, tp, s);
 }
 
 }  // namespace wtp

@@ -56,6 +56,7 @@ constexpr int COLLECT_THREADS = 256; /* k_collect: 4 waves per block ...        
 constexpr int COLLECT_IT = 16;       /* ... of 16 float4 per thread: one CHUNK        */
 constexpr bool COLLECT_WINDOW_INLINE = false; /* window per k_collect block, or one k_window launch */
 constexpr int SEG_PER_LAUNCH = 24;
+constexpr int FB_GROUP = 12;          /* images per filter-bank level launch */
 
 enum SegFlags : int32_t {
     SEG_MASK = 1,      /* level-0 / 1-D: the mask pass writes `out` from `data`   */
@@ -160,8 +161,29 @@ void launch_idwt_rows(const float* a, int64_t a_bs, int64_t lda, int a_from_P, c
                       const float* thr, float* lo, float* hi, hipStream_t s);
 void launch_idwt_cols(const float* lo, const float* hi, int64_t B, int64_t R, int64_t C, const Taps& tp,
                       float* y, int64_t outH, int64_t outW, unsigned long long* zero_count, hipStream_t s);
-/* filterbank.hip: one fused, LDS-tiled launch per level */
+/* filterbank.hip: one fused, LDS-tiled launch per level (and per group of images) */
 bool fb_tiled_ok(int64_t B, int64_t R, int64_t C, const Taps& tp);
+struct FwdItem { /* one image batch's analysis level k: (B, R, C) in -> P details, anext */
+    const float* in;
+    int64_t B, R, C;
+    float* anext;
+    float* P;
+    int64_t PR, PC, offR, offC;
+    int last;
+};
+struct InvItem { /* one image batch's synthesis level k -> y (B, outH, outW) */
+    const float* a_src; /* nullptr: the packed cA */
+    int64_t a_bs, lda;
+    int a_from_P;
+    const float* P;
+    int64_t PR, PC, offR, offC, B, R, C;
+    const float* thr;
+    float* y;
+    int64_t outH, outW;
+    unsigned long long* zc;
+};
+void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s);
+void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s);
 void launch_fwd_level(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* anext, float* P,
                       int64_t PR, int64_t PC, int64_t offR, int64_t offC, int last, hipStream_t s);
 void launch_inv_level(const float* a_src, int64_t a_bs, int64_t lda, int a_from_P, const float* P, int64_t PR,
