@@ -61,7 +61,8 @@ typedef struct wtp_result {
     uint32_t thr32_bits;    /* float32(thr64): the compare of :31 runs in float32    */
     uint32_t max_abs_bits;  /* np.max(np.abs(coeff_arr)) as float32 bits  :29-30     */
     int32_t eff_level;      /* min(level, calculate_max_level(shape))     :64-65     */
-    int32_t path;           /* selection: 1 window candidates, 2 window edges, 3 full scan */
+    int32_t path;           /* selection: 1 window candidates, 2 window edges, 3 full scan;
+                               99 = the resident launch's grid was not co-resident (results invalid) */
 } wtp_result;
 
 /* ---- wavelets ---- */
@@ -132,6 +133,14 @@ int wtp_min_prune_f32(const wtp_tensor* tensors, int ntensors, double fraction, 
  * [2] k_window, [3] k_collect, [4] k_mask_select, [5] inverse DWT done (first segment group).
  * n = 0 disables. */
 int wtp_set_stage_events(void* const* events, int n);
+
+/* Level-0 launch groups whose chunks fit the device's co-resident grid (wtp_resident_capacity
+ * workgroups of 49152 weights, one per CU) run as ONE launch that keeps every weight in
+ * registers between its read and its masked write (k_resident).  It needs the CUs to itself
+ * while it runs; mode 0 always uses the three-launch form (window / collect / mask-select).
+ * Returns the previous mode (process-wide). */
+int wtp_set_resident(int mode);
+int wtp_resident_capacity(void); /* 0 if the current device cannot host the resident launch */
 
 const char* wtp_last_error(void);
 int wtp_last_error_tensor(void); /* index of the tensor that failed validation, or -1 */

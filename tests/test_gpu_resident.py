@@ -1,0 +1,173 @@
+"""GPU parity of the two forms of the level-0 selection: the one-launch resident kernel
+(k_resident: weights held in registers across a grid barrier) and the three-launch form
+(k_window / k_collect / k_mask_select).  Both must equal the C oracle bit for bit (values,
+float64 threshold bits, zero counts) on the same inputs, including the fallbacks (window miss,
+in place) and groups too large for the resident grid."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests import golden_io as G
+
+pytestmark = pytest.mark.gpu
+
+RES_CHUNK = 49152  # weights per resident workgroup (csrc/wtp_internal.h)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from wavelettransforms_amd import engine
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    prev = engine.set_resident(True)
+    yield engine
+    engine.set_resident(prev)
+
+
+@pytest.fixture(params=[True, False], ids=["resident", "three_launch"])
+def mode(request, eng):
+    prev = eng.set_resident(request.param)
+    yield request.param
+    eng.set_resident(prev)
+
+
+def _dev(x):
+    return torch.from_numpy(np.array(x, dtype=np.float32)).cuda()
+
+
+def _same(o, ref, r, rr):
+    assert np.array_equal(o, ref)
+    assert r["zero_count"] == rr["zero_count"]
+    assert G.f64_bits_equal(r["thr64"], rr["thr64"])
+    assert r["eff_level"] == rr["eff_level"]
+
+
+def test_capacity_covers_cfg2(eng):
+    cap = eng.resident_capacity()
+    assert cap >= 232, cap  # 256 CUs on MI355X; cfg2 needs 231 workgroups
+    need = sum(-(-int(np.prod(s)) // RES_CHUNK) for _, s, *_ in G.W.resnet18_tensors(0))
+    assert need <= cap
+
+
+@pytest.mark.parametrize("pct", [0.0, 10.0, 50.0, 78.60000000000001, 100.0])
+def test_cfg2_both_forms_equal_oracle(eng, mode, pct):
+    ts = G.W.resnet18_tensors(0)
+    xs = [eng.synth(s, seed, tid, e) for _, s, seed, tid, e in ts]
+    outs, res = eng.prune(xs, "bior3.3", 5, pct, carry_level=False)
+    for (name, s, seed, tid, e), o, r in zip(ts, outs, res):
+        ref, rr = O.prune_tensor(G.W.synth_numpy(s, seed, tid, e), "bior3.3", 5, pct)
+        _same(o.cpu().numpy(), ref, r, rr)
+        if pct < 100.0:  # pct 100: the window is open above and its buckets overflow -> full scan (path 3)
+            assert r["path"] in (1, 2), (name, r["path"])
+
+
+def test_cfg2_in_place(eng, mode):
+    ts = G.W.resnet18_tensors(0)
+    xs = [eng.synth(s, seed, tid, e) for _, s, seed, tid, e in ts]
+    refs = [O.prune_tensor(x.cpu().numpy(), "bior3.3", 5, 50.0) for x in xs]
+    outs, res = eng.prune(xs, "bior3.3", 5, 50.0, outs=xs, carry_level=False)
+    for x, o, r, (ref, rr) in zip(xs, outs, res, refs):
+        assert o.data_ptr() == x.data_ptr()
+        _same(o.cpu().numpy(), ref, r, rr)
+
+
+def _miss_input(n, seed):
+    """Values whose sampled positions (SAMPLE_GROUP-float groups spread evenly) hold 1.0 while
+    the rest are ~2.0: the sample window misses the true order statistics."""
+    ng, grp = 4096 // 16, 16
+    x = np.full(n, 2.0, np.float32)
+    rng = np.random.default_rng(seed)
+    x += rng.integers(0, 1 << 12, n).astype(np.float32) * np.float32(2.0 ** -20)
+    for g in range(ng):
+        s = int(g * ((n - grp) / (ng - 1)))
+        x[s:s + grp] = 1.0
+    x[::7] *= -1
+    return x
+
+
+@pytest.mark.parametrize("in_place", [False, True], ids=["out_of_place", "in_place"])
+def test_window_miss_full_scan(eng, mode, in_place):
+    n = 300_000
+    x = _miss_input(n, 3)
+    ref, rr = O.prune_tensor(x.reshape(300, 1000), "bior3.3", 0, 37.5)
+    xt = _dev(x).reshape(300, 1000)
+    outs, (r,) = eng.prune([xt], "bior3.3", 0, 37.5, outs=[xt] if in_place else None)
+    assert r["path"] == 3
+    _same(outs[0].cpu().numpy(), ref, r, rr)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4097, RES_CHUNK - 1, RES_CHUNK, RES_CHUNK + 5, 3 * RES_CHUNK + 4099])
+def test_ragged_and_unaligned(eng, mode, n):
+    rng = np.random.default_rng(n)
+    x = (rng.standard_normal(n + 1) * 0.05).astype(np.float32)
+    x[rng.integers(0, n, max(1, n // 50))] = 0.0
+    base = _dev(x)
+    aligned, unaligned = base[:n].clone(), base[1:n + 1]
+    out_u = torch.empty(n + 1, dtype=torch.float32, device=base.device)[1:]
+    outs, res = eng.prune([aligned, unaligned], "db8", 5, 38.2, outs=[torch.empty_like(aligned), out_u],
+                          carry_level=False)
+    for xin, o, r in zip((x[:n], x[1:n + 1]), outs, res):
+        ref, rr = O.prune_tensor(xin.copy(), "db8", 5, 38.2)
+        _same(o.cpu().numpy(), ref, r, rr)
+
+
+def test_nan_and_inf(eng, mode):
+    rng = np.random.default_rng(7)
+    a = (rng.standard_normal(100_000) * 0.05).astype(np.float32)
+    b = a.copy()
+    a[123] = np.nan
+    b[77] = np.inf
+    b[99_000] = -np.inf
+    outs, res = eng.prune([_dev(a), _dev(b)], "db8", 5, 50.0, carry_level=False)
+    for xin, o, r in zip((a, b), outs, res):
+        ref, rr = O.prune_tensor(xin.copy(), "db8", 5, 50.0)
+        assert np.array_equal(o.cpu().numpy(), ref, equal_nan=True)
+        assert r["zero_count"] == rr["zero_count"]
+
+
+def test_ties_and_zeros(eng, mode):
+    """Heavily tied keys (few distinct magnitudes, many exact zeros): counts and masks exact."""
+    rng = np.random.default_rng(11)
+    x = rng.integers(-3, 4, 600_000).astype(np.float32) * np.float32(0.25)
+    for pct in (0.0, 23.599999999999998, 50.0, 61.8, 99.0):
+        outs, (r,) = eng.prune([_dev(x)], "haar", 0, pct)
+        ref, rr = O.prune_tensor(x.copy(), "haar", 0, pct)
+        _same(outs[0].cpu().numpy(), ref, r, rr)
+
+
+def test_more_segments_than_one_group(eng, mode):
+    """30 level-0 tensors: two launch groups back to back (the parity regions alternate)."""
+    shapes = [(64, 64, 3, 3), (128, 64, 1, 1), (256, 32, 3, 3)] * 10
+    xs, refs = [], []
+    for j, s in enumerate(shapes):
+        e = G.W.sigma_exponent(G.W.conv_sigma(s))
+        xs.append(eng.synth(s, 21, j, e))
+        refs.append(O.prune_tensor(G.W.synth_numpy(s, 21, j, e), "bior3.3", 5, 61.8))
+    outs, res = eng.prune(xs, "bior3.3", 5, 61.8, carry_level=False)
+    for o, r, (ref, rr) in zip(outs, res, refs):
+        _same(o.cpu().numpy(), ref, r, rr)
+
+
+def test_group_larger_than_resident_grid_falls_back(eng):
+    """A level-0 group needing more workgroups than resident_capacity() runs the three-launch
+    form (same results)."""
+    cap = eng.resident_capacity()
+    n = (cap + 8) * RES_CHUNK
+    x = eng.synth((n,), 31, 0, 27)
+    outs, (r,) = eng.prune([x], "haar", 0, 50.0)
+    ref, rr = O.prune_tensor(x.cpu().numpy(), "haar", 0, 50.0)
+    _same(outs[0].cpu().numpy(), ref, r, rr)
+
+
+def test_alternating_forms_share_the_workspace(eng):
+    """Resident and three-launch calls interleaved on one workspace: each leaves the parity
+    regions clean for the other."""
+    ts = G.W.resnet18_tensors(0)[:8]
+    xs = [eng.synth(s, seed, tid, e) for _, s, seed, tid, e in ts]
+    first, r0 = eng.prune(xs, "bior3.3", 5, 50.0, carry_level=False)
+    for k in range(6):
+        eng.set_resident(k % 2 == 0)
+        outs, res = eng.prune(xs, "bior3.3", 5, 50.0, carry_level=False)
+        for a, b, ra, rb in zip(first, outs, r0, res):
+            assert torch.equal(a, b) and ra["zero_count"] == rb["zero_count"]
+    eng.set_resident(True)

@@ -75,6 +75,8 @@ def lib():
             "wtp_set_stage_events": ([ctypes.POINTER(ctypes.c_void_p), i32], i32),
             "wtp_min_prune_workspace_size": ([tp, i32, f64], sz),
             "wtp_min_prune_f32": ([tp, i32, f64, vp, sz, vp, vp], i32),
+            "wtp_set_resident": ([i32], i32),
+            "wtp_resident_capacity": ([], i32),
             "wtp_last_error": ([], ctypes.c_char_p),
             "wtp_last_error_tensor": ([], i32),
         }

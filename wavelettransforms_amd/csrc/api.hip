@@ -5,6 +5,7 @@
  * stream-ordered and graph-capturable.
  */
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -23,6 +24,7 @@ thread_local std::string g_err;
 thread_local int g_err_tensor = -1;
 thread_local hipEvent_t g_stage_ev[8];
 thread_local int g_stage_n = 0;
+std::atomic<int> g_resident{1}; /* wtp_set_resident */
 
 inline void stage(int i, hipStream_t s) {
     if (i < g_stage_n && g_stage_ev[i]) (void)hipEventRecord(g_stage_ev[i], s);
@@ -90,9 +92,11 @@ constexpr size_t PERSIST_BYTES = ((sizeof(SelHeader) + 2 * SEL_REGION) + 255) / 
 
 bool pct_ok(double pct) { return pct >= 0.0 && pct <= 100.0; }
 
-/* candidate buckets: the sample window holds ~3.6% of a large population (6-sigma margins at
- * 32768 samples); size the bucket count for ~1000 expected keys each and give every bucket
- * ~4x headroom (an overflowing bucket sends k_select to its exact full-scan path). */
+/* candidate buckets of the three-launch form: ~1000 keys of 5% of the population per bucket
+ * (64..1024 buckets; the window holds ~11%, so ~2000) -- long runs per block keep k_collect's
+ * scatter in whole lines -- with capacity for 4x that (an overflowing bucket sends the select
+ * to its exact full-scan path).  The resident form always uses NSUB_MAX buckets: its runs are
+ * per workgroup, and narrow buckets let one LDS histogram finish the select. */
 void bucket_plan(int64_t n, int* nsub_log2, int* bucket_cap) {
     const double expect = 0.05 * (double)n;
     int lg = 6;
@@ -180,6 +184,11 @@ Layout make_layout(std::vector<TPlan>& ps) {
     L.cand = off;
     size_t ce = 0;
     for (auto& p : ps) { p.cand_off = ce; ce += (size_t)p.cap; }
+    /* a resident launch (k_resident) keeps one run of RES_WG_WORDS per workgroup there instead */
+    int64_t rwg = 0;
+    for (auto& p : ps)
+        if (!p.dwt) rwg += (p.pop + RES_CHUNK - 1) / RES_CHUNK;
+    ce = std::max(ce, (size_t)std::min<int64_t>(rwg, RES_MAX_WG) * RES_WG_WORDS);
     off = align_up(off + ce * sizeof(uint32_t));
     L.P = off;
     for (auto& p : ps) {
@@ -345,6 +354,12 @@ int wtp_set_stage_events(void* const* events, int n) {
     return WTP_OK;
 }
 int wtp_last_error_tensor(void) { return g_err_tensor; }
+int wtp_set_resident(int mode) {
+    if (mode < 0 || mode > 1) return fail(WTP_EARG, -1, "bad resident mode %d", mode);
+    const int prev = g_resident.exchange(mode);
+    return prev;
+}
+int wtp_resident_capacity(void) { return resident_capacity(); }
 
 size_t wtp_workspace_size(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level) {
     if (ntensors < 0 || (ntensors > 0 && !tensors)) return 0;
@@ -400,12 +415,24 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             return fail(WTP_EHIP, t, "hipMemsetAsync failed");
     }
     forward_chains(chains, tp, s);
-    /* 2. exact percentile selection + level-0 mask, SEG_PER_LAUNCH segments per launch group */
+    /* 2. exact percentile selection + level-0 mask, SEG_PER_LAUNCH segments per launch group:
+     * one resident launch when every segment of the group is level-0 and the group's chunks fit
+     * the co-resident grid, else window / collect / mask-select */
     for (int g0 = 0; g0 < ntensors; g0 += SEG_PER_LAUNCH) {
+        const int g1 = std::min(ntensors, g0 + SEG_PER_LAUNCH);
+        bool all0 = true;
+        int64_t rblk = 0;
+        for (int t = g0; t < g1; ++t) {
+            all0 = all0 && !ps[t].dwt;
+            rblk += (ps[t].pop + RES_CHUNK - 1) / RES_CHUNK;
+        }
+        const bool resident = all0 && g_resident.load(std::memory_order_relaxed) && rblk <= RES_MAX_WG &&
+                              rblk <= resident_capacity();
+        const int64_t chunk = resident ? RES_CHUNK : CHUNK;
         SegTable tab;
         memset(&tab, 0, sizeof tab);
         int blk = 0;
-        for (int t = g0; t < ntensors && t < g0 + SEG_PER_LAUNCH; ++t) {
+        for (int t = g0; t < g1; ++t) {
             const TPlan& p = ps[t];
             SegDesc& sd = tab.s[tab.nseg++];
             sd.data = p.dwt ? reinterpret_cast<const float*>(wsb(ws, p.p_off)) : tensors[t].in;
@@ -424,17 +451,26 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             sd.cand_off = (int64_t)p.cand_off;
             sd.cap = p.cap;
             bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap);
-            blk += (int)((p.pop + CHUNK - 1) / CHUNK);
+            if (resident) sd.nsub_log2 = 10; /* NSUB_MAX */
+            blk += (int)((p.pop + chunk - 1) / chunk);
         }
         tab.nblk = blk;
         for (int i = tab.nseg; i < SEG_PER_LAUNCH; ++i) tab.blk_begin[i] = INT32_MAX;
         const bool first = g0 == 0;
         if (first) stage(1, s);
-        launch_window(tab, head, s);
-        if (first) stage(2, s);
-        launch_collect(tab, head, cand, results, s);
-        if (first) stage(3, s);
-        launch_mask_select(tab, head, cand, results, thr_t, s);
+        if (resident) {
+            if (first) { stage(2, s); stage(3, s); }
+            launch_resident(tab, head, cand, results, thr_t, s);
+        } else {
+            launch_window(tab, head, s);
+            if (first) stage(2, s);
+            launch_collect(tab, head, cand, results, s);
+            if (first) stage(3, s);
+            launch_mask_select(tab, head, cand, results, thr_t, s);
+            bool inplace = false;
+            for (int i = 0; i < tab.nseg; ++i) inplace = inplace || (tab.s[i].out && tab.s[i].out == tab.s[i].data);
+            if (inplace) launch_mask_inplace(tab, results, thr_t, s);
+        }
         if (first) stage(4, s);
     }
     /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2) */

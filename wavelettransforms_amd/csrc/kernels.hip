@@ -22,12 +22,30 @@
 #include "wtp_internal.h"
 #include "wt_synth.h"
 
+#include <atomic>
+#include <cstdlib>
+
 #pragma clang fp contract(off)
 
 namespace wtp {
 
 /* ---------------------------------------------------------------- helpers --- */
 __device__ __forceinline__ uint32_t abs_key(float x) { return __float_as_uint(x) & 0x7FFFFFFFu; }
+
+/* Loads and stores of bytes handed between workgroups of ONE launch (k_resident): agent-scope
+ * relaxed atomics lower to global_load/store ... sc1, which bypass the CU's L1 and write
+ * through the XCD's L2 (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores + sc1 loads
+ * + an agent-scope arrival counter, one workgroup per CU).  COH = false: plain accesses (the
+ * data was produced by an earlier launch). */
+template <bool COH, class T>
+__device__ __forceinline__ T ldc(const T* p) {
+    if constexpr (COH) return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <class T>
+__device__ __forceinline__ void stc(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ int find_seg(const SegTable& t, int b) {
     int s = 0; /* blk_begin[0] == 0; entries past nseg hold INT32_MAX */
@@ -119,6 +137,26 @@ __device__ __forceinline__ void load_chunk_ragged(const float* p, int len, float
         v[it].w = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e + 12, 0, 0));
     }
 }
+/* range-checked float4 store: the dwords past the buffer's length are dropped */
+__device__ __forceinline__ void store4_ragged(const float4& y, __amdgpu_buffer_rsrc_t r, int off) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y.x), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y.y), r, off + 4, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y.z), r, off + 8, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y.w), r, off + 12, 0, 0);
+}
+/* a copy the compiler cannot see through: keys derived from it are recomputed where needed
+ * instead of being kept live beside the data (k_resident holds 96 floats per thread) */
+__device__ __forceinline__ float opaque(float x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+/* float4 slot j of a partial chunk of len elements: whole float4 stores where the slot is
+ * complete and the buffer 16-byte aligned, range-checked dword stores otherwise */
+__device__ __forceinline__ void store4_tail(const float4& y, float* q, __amdgpu_buffer_rsrc_t r, int j, int len,
+                                            bool aligned) {
+    if (aligned && 4 * j + 3 < len) reinterpret_cast<float4*>(q)[j] = y;
+    else if (4 * j < len) store4_ragged(y, r, 16 * j);
+}
 __device__ __forceinline__ float f4_get(const float4& v, int c) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); }
 
 /* --------------------------------------------------------- radix select --- */
@@ -145,6 +183,15 @@ __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, i
 #endif
 #ifndef WTP_CPROBE
 #define WTP_CPROBE(i)
+#endif
+#ifndef WTP_RPROBE
+#define WTP_RPROBE(i)
+#endif
+#ifndef WTP_WPROBE
+#define WTP_WPROBE(i)
+#endif
+#ifndef WTP_RES_ABL /* tools/mb/reslab.hip ablations: bit 0 window, 1 count, 2 bucket scatter, 3 select, 4 barrier */
+#define WTP_RES_ABL 0
 #endif
 
 /* ------------------------------------------------------------ the window --- */
@@ -192,42 +239,50 @@ __device__ __forceinline__ void window_from_keys(const SegDesc& sd, const uint32
     for (int i = threadIdx.x; i < FBP * THREADS; i += THREADS) L.h[i] = 0;
     if (threadIdx.x < 2) L.found[threadIdx.x] = -1;
     __syncthreads();
+    WTP_WPROBE(0);
 #pragma unroll
     for (int j = 0; j < PER; ++j)
         if (j * THREADS + (int)threadIdx.x < m) atomicAdd(&L.h[key_bin(k[j])], 1u);
     __syncthreads();
+    WTP_WPROBE(1);
+    /* sample ranks fit 32 bits; the bin counts stay in registers from the scan to the search */
     const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
-    int64_t sa, sb;
+    int sa, sb;
     if (exact) {
-        sa = r0;
-        sb = r1;
+        sa = (int)r0;
+        sb = (int)r1;
     } else {
         const double p = (double)r0 / (double)(n - 1);
         const double s0 = p * (double)(m - 1), s1 = (double)r1 / (double)(n - 1) * (double)(m - 1);
         const double d = 6.0 * sqrt((double)m * p * (1.0 - p)) + 24.0;
-        sa = (int64_t)floor(s0 - d);
-        sb = (int64_t)ceil(s1 + d);
+        sa = (int)floor(s0 - d);
+        sb = (int)ceil(s1 + d);
     }
+    uint32_t c[FBP];
+#pragma unroll
+    for (int j = 0; j < FBP; ++j) c[j] = L.h[threadIdx.x * FBP + j];
     uint32_t local = 0;
 #pragma unroll
-    for (int j = 0; j < FBP; ++j) local += L.h[threadIdx.x * FBP + j];
+    for (int j = 0; j < FBP; ++j) local += c[j];
     const uint32_t incl = wave_scan_u32(local);
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 63) L.wtot[wv] = incl;
     __syncthreads();
-    int64_t cum = (int64_t)incl - local;
-    for (int i = 0; i < wv; ++i) cum += L.wtot[i];
+    WTP_WPROBE(2);
+    int cum = (int)(incl - local);
 #pragma unroll
-    for (int j = 0; j < FBP; ++j) {
-        const int b = threadIdx.x * FBP + j;
-        const int64_t c = L.h[b];
-        if (c) {
-            if (sa >= cum && sa < cum + c) L.found[0] = b;
-            if (sb >= cum && sb < cum + c) L.found[1] = b;
+    for (int i = 0; i < THREADS / 64; ++i) cum += i < wv ? (int)L.wtot[i] : 0;
+    if (sa >= cum || sb >= cum) { /* only threads at or below the ranks search their bins */
+#pragma unroll
+        for (int j = 0; j < FBP; ++j) {
+            const int nx = cum + (int)c[j];
+            if (sa >= cum && sa < nx) L.found[0] = threadIdx.x * FBP + j;
+            if (sb >= cum && sb < nx) L.found[1] = threadIdx.x * FBP + j;
+            cum = nx;
         }
-        cum += c;
     }
     __syncthreads();
+    WTP_WPROBE(3);
     const int f0 = L.found[0], f1 = L.found[1];
     const uint32_t kl = (sa < 0 || f0 < 0) ? 0u : bin_lo_key(f0);
     const uint32_t kh = (sb >= m || f1 < 0) ? 0xFFFFFFFFu : bin_hi_key(f1);
@@ -336,11 +391,18 @@ __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __rest
     for (uint32_t i = 0; i < cnt; ++i) atomicAdd(&lsub[(stage[i * CT + threadIdx.x] - kl - 1) >> sh], 1u);
     __syncthreads();
     if (LAB == 2) return;
-    /* reserve one contiguous run per non-empty bucket (one returning atomic per bucket) */
-    for (int b = threadIdx.x; b < nsub; b += CT) {
-        const uint32_t c = lsub[b];
-        lbase[b] = c ? atomicAdd(&st->sub[b], c) : 0u;
-        lsub[b] = 0;
+    /* reserve one contiguous run per non-empty bucket (one returning atomic per bucket, all of a
+     * thread's in flight at once) */
+    {
+        constexpr int PER = NSUB_MAX / CT;
+        uint32_t cj[PER], rj[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) cj[j] = (j * CT + (int)threadIdx.x < nsub) ? lsub[j * CT + threadIdx.x] : 0u;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) rj[j] = cj[j] ? atomicAdd(&st->sub[j * CT + threadIdx.x], cj[j]) : 0u;
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+            if (j * CT + (int)threadIdx.x < nsub) { lbase[j * CT + threadIdx.x] = rj[j]; lsub[j * CT + threadIdx.x] = 0; }
     }
     __syncthreads();
     WTP_CPROBE(4);
@@ -397,6 +459,73 @@ __device__ void select_in_range(const Get& get, const Keep& keep, int64_t m, uin
     *kb = pb;
 }
 
+/* Rank r (0-based, ascending) among the m <= 64*KPL keys stage[0..m), all in [lo, hi]; one
+ * wave, keys in registers.  Bit by bit below the common prefix of lo and hi, the result takes a
+ * bit when at most r keys lie below it: it ends at the largest t with #(key < t) <= r, which is
+ * the r-th key itself.  Every lane of the wave must be active. */
+constexpr int WSEL_KPL = 16;
+constexpr int STAGE_BATCH = 4;
+template <int KPL>
+__device__ __forceinline__ uint32_t wave_select_rank(const uint32_t* stage, int m, int64_t r, uint32_t lo, uint32_t hi) {
+    const int lane = threadIdx.x & 63;
+    uint32_t k[KPL];
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+        const int i = j * 64 + lane;
+        k[j] = i < m ? stage[i] : 0xFFFFFFFFu; /* above every |x| key */
+    }
+    const uint32_t diff = lo ^ hi;
+    const int top = diff ? 31 - __clz(diff) : -1;
+    uint32_t res = top >= 31 ? 0u : (lo & ~((2u << top) - 1u));
+    const uint32_t rr = (uint32_t)r; /* r < m */
+    for (int b = top; b >= 0; --b) {
+        const uint32_t cand = res | (1u << b);
+        uint32_t c = 0; /* counted on the scalar unit: compare masks and popcounts, no DPP chain */
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) c += (uint32_t)__popcll(__ballot(k[j] < cand));
+        if (c <= rr) res = cand;
+    }
+    return res;
+}
+
+/* Ranks ra / rb among the m keys stage[0..m), all in [lo, lo + W), W <= HS_PER * THREADS:
+ * one LDS histogram over the W key values, a block scan of per-thread runs of HS_PER bins kept
+ * in registers, and the thread whose run holds a rank names its key.  out[] and wt[] are LDS. */
+constexpr int HS_PER = 16;
+template <int THREADS>
+__device__ __forceinline__ void block_hist_select(const uint32_t* stage, int m, uint32_t lo, int W, int ra, int rb,
+                                                  uint32_t* hist, uint32_t* out, uint32_t* wt) {
+    const int per = (W + THREADS - 1) / THREADS;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    for (int i = tid; i < per * THREADS; i += THREADS) hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < m; i += THREADS) atomicAdd(&hist[stage[i] - lo], 1u);
+    __syncthreads();
+    uint32_t c[HS_PER];
+    uint32_t local = 0;
+#pragma unroll
+    for (int j = 0; j < HS_PER; ++j) {
+        c[j] = j < per ? hist[tid * per + j] : 0u;
+        local += c[j];
+    }
+    const uint32_t incl = wave_scan_u32(local);
+    if (lane == 63) wt[wv] = incl;
+    __syncthreads();
+    int cum = (int)(incl - local);
+#pragma unroll
+    for (int i = 0; i < THREADS / 64; ++i) cum += i < wv ? (int)wt[i] : 0;
+    if (local && ((ra >= cum && ra < cum + (int)local) || (rb >= cum && rb < cum + (int)local))) {
+#pragma unroll
+        for (int j = 0; j < HS_PER; ++j) {
+            const int nx = cum + (int)c[j];
+            if (ra >= cum && ra < nx) out[0] = lo + (uint32_t)(tid * per + j);
+            if (rb >= cum && rb < nx) out[1] = lo + (uint32_t)(tid * per + j);
+            cum = nx;
+        }
+    }
+    __syncthreads();
+}
+
 /* count of keys < tk among get(i), block-wide; valid in every thread */
 template <int THREADS, class Get>
 __device__ int64_t block_count_below(const Get& get, int64_t m, uint32_t tk) {
@@ -413,19 +542,47 @@ __device__ int64_t block_count_below(const Get& get, int64_t m, uint32_t tk) {
     return r;
 }
 
-__device__ __forceinline__ void wave_find_bucket(const uint32_t* sub, int nsub, int64_t r, int* bucket,
-                                                 int64_t* before) {
+/* The buckets holding ranks ra / rb from the counts in LDS: lane l takes the nsub/64
+ * consecutive buckets from l * per (ds_read_b128), one wave scan of the lane sums, a ballot for
+ * the lane, then a walk over that lane's buckets.  Writes bucket[i] and before[i] (the keys in
+ * the buckets below it). */
+__device__ __forceinline__ void wave_find_buckets(const uint32_t* lsub, int nsub, bool need_a, int64_t ra, bool need_b,
+                                                  int64_t rb, int* bucket, int64_t* before) {
     const int lane = threadIdx.x & 63;
-    const int per = nsub / 64; /* 1..16 consecutive buckets per lane */
-    uint32_t s = 0; /* bucket counts of one segment: < 2^32 */
-    for (int j = 0; j < per; ++j) s += sub[lane * per + j];
-    const int64_t incl = wave_scan_u32(s);
-    int64_t cum = incl - s;
-    if (r >= cum && r < incl) {
-        for (int j = 0; j < per; ++j) {
-            const int64_t c = sub[lane * per + j];
-            if (r < cum + c) { *bucket = lane * per + j; *before = cum; break; }
-            cum += c;
+    const int per = nsub / 64; /* 1..16 */
+    uint32_t c[16];
+    const uint4* p4 = reinterpret_cast<const uint4*>(lsub + lane * per);
+    if (per >= 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 t = q < per / 4 ? p4[q] : make_uint4(0u, 0u, 0u, 0u);
+            c[4 * q] = t.x; c[4 * q + 1] = t.y; c[4 * q + 2] = t.z; c[4 * q + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) c[q] = q < per ? lsub[lane * per + q] : 0u;
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += c[q];
+    const uint32_t incl = wave_scan_u32(s);
+    const int64_t excl = (int64_t)(incl - s);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        if (!(i == 0 ? need_a : need_b)) continue; /* uniform */
+        const int64_t r = i == 0 ? ra : rb;
+        const bool hit = excl <= r && r < (int64_t)incl;
+        if (hit) { /* one lane: walk its buckets */
+            int64_t cum = excl;
+            int b = lane * per;
+            bool go = true;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                go = go && q < per && r >= cum + (int64_t)c[q];
+                if (go) { cum += c[q]; ++b; }
+            }
+            bucket[i] = b;
+            before[i] = cum;
         }
     }
 }
@@ -433,10 +590,11 @@ __device__ __forceinline__ void wave_find_bucket(const uint32_t* sub, int nsub, 
 /* Resolve the two order statistics of one segment from its counters and buckets, compute the
  * NumPy threshold and the level-0 zero count, publish the results, and leave the slot clean.
  * One block of THREADS threads; `stage` holds up to stage_cap keys in LDS. */
-template <int THREADS>
+template <int THREADS, bool COH = false>
 __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st, const uint32_t* __restrict__ cand,
                              wtp_result* __restrict__ res, float* __restrict__ thr_out, uint32_t* stage,
-                             int stage_cap, bool publish) {
+                             int stage_cap, bool publish, uint32_t kl, uint32_t kh, uint32_t sh,
+                             int* path_out = nullptr, uint32_t* hscratch = nullptr, const ResRuns* rr = nullptr) {
     __shared__ int sbin[2];
     __shared__ int64_t sbefore[2];
     __shared__ uint32_t lsub[NSUB_MAX];
@@ -444,7 +602,6 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
     __shared__ uint32_t s_mk, s_ovf;
     const int nsub = 1 << sd.nsub_log2;
     const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
-    const uint32_t kl = st->kl, kh = st->kh, sh = st->shift;
     WTP_PROBE(0);
     /* one round trip: threads 0..4 gather the sharded counters, wave 1 the bucket counts (to LDS) */
     if (threadIdx.x < 64) {
@@ -453,20 +610,30 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
             const unsigned long long* a = l == 0 ? st->below : (l == 1 ? st->eq_lo : st->eq_hi);
             unsigned long long v = 0;
 #pragma unroll
-            for (int i = 0; i < NSHARD; ++i) v += a[i];
+            for (int i = 0; i < NSHARD; ++i) v += ldc<COH>(a + i);
             s_cnt[l] = v;
         } else if (l == 3) {
             uint32_t m = 0;
 #pragma unroll
-            for (int i = 0; i < NSHARD; ++i) m = max(m, st->maxkey[i]);
+            for (int i = 0; i < NSHARD; ++i) m = max(m, ldc<COH>(st->maxkey + i));
             s_mk = m;
         } else if (l == 4) {
-            s_ovf = st->overflow;
+            s_ovf = ldc<COH>(&st->overflow);
         }
-    } else if (threadIdx.x < 128) {
+    }
+    /* wave 1: the bucket counts (bucket j * 64 + lane in sv[j]), every load issued before the
+     * first is used -- 16 in flight per lane at nsub 1024, not 16 round trips in a row */
+    uint32_t sv[NSUB_MAX / 64];
+    if (threadIdx.x >= 64 && threadIdx.x < 128) {
         const int l = threadIdx.x - 64;
+#pragma unroll
+        for (int j = 0; j < NSUB_MAX / 64; ++j) sv[j] = (j * 64 + l < nsub) ? ldc<COH>(st->sub + j * 64 + l) : 0u;
         uint32_t sm = 0;
-        for (int b = l; b < nsub; b += 64) { const uint32_t v = st->sub[b]; lsub[b] = v; sm += v; }
+#pragma unroll
+        for (int j = 0; j < NSUB_MAX / 64; ++j) {
+            if (j * 64 + l < nsub) lsub[j * 64 + l] = sv[j];
+            sm += sv[j];
+        }
         sm = wave_sum_u32(sm);
         if (l == 0) s_cnt[3] = sm;
     }
@@ -498,8 +665,8 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
     bool in_lds = false;
     bool full = ca == 0 || cb == 0 || s_ovf != 0;
     if (!full && (ca == 2 || cb == 2)) {
-        if (threadIdx.x < 64 && ca == 2) wave_find_bucket(lsub, nsub, ja, &sbin[0], &sbefore[0]);
-        if (threadIdx.x >= 64 && threadIdx.x < 128 && cb == 2) wave_find_bucket(lsub, nsub, jb, &sbin[1], &sbefore[1]);
+        if (threadIdx.x >= 64 && threadIdx.x < 128) /* wave 1: both ranks from one scan */
+            wave_find_buckets(lsub, nsub, ca == 2, ja, cb == 2, jb, sbin, sbefore);
         __syncthreads();
         WTP_PROBE(2);
         blo = (ca == 2) ? sbin[0] : sbin[1];
@@ -508,24 +675,95 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
         /* adjacent ranks: buckets strictly between blo and bhi are empty */
         nlo = lsub[blo];
         nhi = (bhi != blo) ? lsub[bhi] : 0;
-        if (nlo > bcap || nhi > bcap) {
+        if (rr ? nlo + nhi > stage_cap : (nlo > bcap || nhi > bcap)) {
             full = true;
-        } else {
-            in_lds = nlo + nhi <= stage_cap;
-            if (in_lds) {
-                for (int i = threadIdx.x; i < nlo; i += THREADS) stage[i] = c[(int64_t)blo * bcap + i];
-                for (int i = threadIdx.x; i < nhi; i += THREADS) stage[nlo + i] = c[(int64_t)bhi * bcap + i];
+        } else if (rr) {
+            /* k_resident: bucket blo (then bhi) is spread over the runs of the segment's workgroups:
+             * one thread per (run, bucket) reads the run's two offsets, a block scan places the
+             * pieces, every thread copies its piece */
+            in_lds = true;
+            __shared__ uint32_t gwt[THREADS / 64];
+            const int t = threadIdx.x, nw = rr->nw;
+            const int nrun = bhi != blo ? 2 * nw : nw;
+            uint32_t cnt = 0;
+            const uint32_t* src = nullptr;
+            if (t < nrun) {
+                const int w = t < nw ? t : t - nw;
+                const int b = t < nw ? blo : bhi;
+                const uint32_t* run = rr->base + (int64_t)(rr->wb + w) * RES_WG_WORDS;
+                const uint32_t o0 = ldc<true>(run + b), o1 = ldc<true>(run + b + 1);
+                cnt = o1 - o0;
+                src = run + RES_OFF_WORDS + o0;
+            }
+            const uint32_t incl = wave_scan_u32(cnt);
+            if ((t & 63) == 63) gwt[t >> 6] = incl;
+            __syncthreads();
+            uint32_t dst = incl - cnt;
+            for (int w = 0; w < (t >> 6); ++w) dst += gwt[w];
+            for (uint32_t j0 = 0; j0 < cnt; j0 += 4) {
+                uint32_t kk[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) kk[q] = j0 + q < cnt ? ldc<true>(src + j0 + q) : 0u;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (j0 + q < cnt) stage[dst + j0 + q] = kk[q];
+            }
+            __syncthreads();
+        }
+        if (!full) {
+            if (!rr) in_lds = nlo + nhi <= stage_cap;
+            if (in_lds && !rr) { /* STAGE_BATCH loads in flight per thread before any is used */
+                const int64_t m = nlo + nhi;
+                for (int64_t i0 = 0; i0 < m; i0 += (int64_t)THREADS * STAGE_BATCH) {
+                    uint32_t v[STAGE_BATCH];
+#pragma unroll
+                    for (int j = 0; j < STAGE_BATCH; ++j) {
+                        const int64_t i = i0 + (int64_t)j * THREADS + threadIdx.x;
+                        v[j] = i < m ? ldc<COH>(i < nlo ? c + (int64_t)blo * bcap + i : c + (int64_t)bhi * bcap + i - nlo)
+                                     : 0u;
+                    }
+#pragma unroll
+                    for (int j = 0; j < STAGE_BATCH; ++j) {
+                        const int64_t i = i0 + (int64_t)j * THREADS + threadIdx.x;
+                        if (i < m) stage[i] = v[j];
+                    }
+                }
                 __syncthreads();
             }
             WTP_PROBE(3);
             const uint64_t lo64 = (uint64_t)kl + 1 + ((uint64_t)blo << sh);
             const uint64_t hi64 = min((uint64_t)kh, (uint64_t)kl + ((uint64_t)(bhi + 1) << sh));
             uint32_t xa = 0, xb = 0;
-            auto getb = [&](int64_t i) {
-                return in_lds ? stage[i] : (i < nlo ? c[(int64_t)blo * bcap + i] : c[(int64_t)bhi * bcap + i - nlo]);
-            };
-            select_in_range<THREADS>(getb, [](uint32_t) { return true; }, nlo + nhi, (uint32_t)lo64,
-                                     (uint32_t)hi64, ja - before, jb - before, ca == 2, cb == 2, &xa, &xb);
+            if (in_lds && hscratch && hi64 - lo64 < (uint64_t)(HS_PER * THREADS)) {
+                /* one LDS histogram over the bucket's key values: both ranks in one pass */
+                __shared__ uint32_t sx[2], wt[THREADS / 64];
+                block_hist_select<THREADS>(stage, (int)(nlo + nhi), (uint32_t)lo64, (int)(hi64 - lo64 + 1),
+                                           (int)(ja - before), (int)(jb - before), hscratch, sx, wt);
+                xa = sx[0];
+                xb = sx[1];
+            } else if (in_lds && nlo + nhi <= 64 * WSEL_KPL) {
+                /* a few hundred keys: one wave per rank, a bitwise search in registers */
+                __shared__ uint32_t sx[2];
+                const int wv = threadIdx.x >> 6;
+                if (wv == 0 && ca == 2) {
+                    const uint32_t k = wave_select_rank<WSEL_KPL>(stage, (int)(nlo + nhi), ja - before, (uint32_t)lo64, (uint32_t)hi64);
+                    if ((threadIdx.x & 63) == 0) sx[0] = k;
+                }
+                if (wv == 1 && cb == 2) {
+                    const uint32_t k = wave_select_rank<WSEL_KPL>(stage, (int)(nlo + nhi), jb - before, (uint32_t)lo64, (uint32_t)hi64);
+                    if ((threadIdx.x & 63) == 0) sx[1] = k;
+                }
+                __syncthreads();
+                xa = sx[0];
+                xb = sx[1];
+            } else {
+                auto getb = [&](int64_t i) {
+                    return in_lds ? stage[i]
+                                  : ldc<COH>(i < nlo ? c + (int64_t)blo * bcap + i : c + (int64_t)bhi * bcap + i - nlo);
+                };
+                select_in_range<THREADS>(getb, [](uint32_t) { return true; }, nlo + nhi, (uint32_t)lo64,
+                                         (uint32_t)hi64, ja - before, jb - before, ca == 2, cb == 2, &xa, &xb);
+            }
             ka = (ca == 2) ? xa : (ca == 1 ? kl : kh);
             kb = (cb == 2) ? xb : (cb == 1 ? kl : kh);
             path = MODE_CAND;
@@ -556,6 +794,7 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
      * adjacent, so #(key < tk) = below + [tk > kl] eq_lo + before + #(staged < tk).  A NaN
      * threshold prunes nothing: every k_mask_select block counts the zeros of its copy. */
     WTP_PROBE(5);
+    if (path_out) *path_out = path;
     if (!publish) return minp ? __uint_as_float(ka) : thr32; /* block-uniform */
     int64_t zc = 0;
     /* min pruning (k_minsel) wants #(key < t) for the exact key t = ka: none when t == 0 */
@@ -568,7 +807,8 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
                  block_count_below<THREADS>(
                      [&](int64_t i) {
                          return in_lds ? stage[i]
-                                       : (i < nlo ? c[(int64_t)blo * bcap + i] : c[(int64_t)bhi * bcap + i - nlo]);
+                                       : ldc<COH>(i < nlo ? c + (int64_t)blo * bcap + i
+                                                          : c + (int64_t)bhi * bcap + i - nlo);
                      },
                      nlo + nhi, tk);
         else
@@ -586,7 +826,8 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
         r.thr32_bits = __float_as_uint(thr32);
         r.max_abs_bits = mk;
         r.eff_level = sd.eff_level;
-        r.path = path;
+        if constexpr (COH) atomicMax(&r.path, path); /* a timed-out workgroup may raise it to MODE_FAULT */
+        else r.path = path;
     }
     WTP_PROBE(6);
     return minp ? __uint_as_float(ka) : thr32;
@@ -721,8 +962,13 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_mask_select(SegTable t, cons
      * the select's would only delay its round trips -- and the chunk's 64 registers would sit
      * live through it */
     const SelState* st = sel_region(const_cast<SelHeader*>(head), head->parity ^ 1u) + sd.slot;
-    const float thr = select_body<STREAM_THREADS>(sd, st, cand, res, thr_out, stage, MS_STAGE, base == 0);
+    int path = 0;
+    const float thr = select_body<STREAM_THREADS>(sd, st, cand, res, thr_out, stage, MS_STAGE, base == 0, st->kl,
+                                                  st->kh, st->shift, &path);
     if (!masked) return;
+    /* a full-scan select reads the whole segment: in place, no block of it may write before
+     * every block has scanned -- k_mask_inplace writes it in the next launch */
+    if (path == MODE_FULL && sd.data == sd.out) return;
     float4 v[16];
     {
         const float* p = sd.data + base;
@@ -763,6 +1009,323 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_mask_select(SegTable t, cons
     }
 }
 
+/* ------------------------------------------------------------- k_resident --- */
+/* The level-0 prune of a whole launch group in ONE launch.  Every workgroup is resident (one per
+ * CU; the host checks the grid against resident_capacity()) and holds its chunk in VGPRs from
+ * the first read to the masked write, so HBM sees 4 B read + 4 B written per weight -- the
+ * algorithmic minimum -- and the selection's two dependent steps run between them:
+ *   P0  the sample loads, then the chunk's loads (RES_IT float4 per thread); the segment's
+ *       window is built from the sample while the chunk is in flight (every workgroup of a
+ *       segment draws the same sample and derives the same window)
+ *   P1  from registers: count keys < kl and == kl, max key; histogram the keys inside (kl, kh]
+ *       over the buckets in LDS, reserve one run per non-empty bucket (returning atomic), re-scan
+ *       the registers and scatter the inside keys with write-through (sc1) stores
+ *   --  grid barrier: each workgroup's waves drain their stores (vmcnt(0)), lane 0 adds to its
+ *       shard's arrival counter (blockIdx % 8), wave 0 polls all shards with sc1 loads
+ *   P2  every workgroup resolves its segment's threshold (select_body over sc1 loads); the
+ *       segment's first workgroup publishes the record and the exact zero count
+ *   P3  out = where(|x| < thr, 0, x) from registers
+ * A segment whose window missed is re-scanned from memory (full radix select); when its input is
+ * also its output (in place) its workgroups meet at a segment-wide barrier before any writes.
+ * Every wait is bounded (RES_TIMEOUT of the 100 MHz wall clock): a grid that is not co-resident
+ * after all drains instead of hanging, and its records read MODE_FAULT. */
+constexpr uint64_t RES_TIMEOUT_TICKS = 20000000ull; /* 200 ms */
+constexpr int RES_STG = 32;                         /* inside keys a thread may stage (of its 96; ~11 expected) */
+
+__device__ __forceinline__ uint64_t wall_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
+/* Wave 0 waits until every shard counter has reached its expected arrivals (expect(lane));
+ * block-uniform result: false on timeout. */
+template <class Expect>
+__device__ __forceinline__ bool res_wait(const uint32_t* ctr, int stride, const Expect& expect, int nctr) {
+    __shared__ int s_ok;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        const uint32_t want = lane < nctr ? expect(lane) : 0u;
+        const uint64_t t0 = wall_ticks();
+        bool ok = true;
+        while (true) {
+            const uint32_t v = lane < nctr ? ldc<true>(ctr + lane * stride) : 0u;
+            if (__all(v >= want)) break;
+            if (wall_ticks() - t0 > RES_TIMEOUT_TICKS) { ok = false; break; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (lane == 0) s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+template <bool FULL, bool SPEC>
+__device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, SelHeader* __restrict__ head, uint32_t q,
+                                         uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
+                                         float* __restrict__ thr_out, int64_t base, int len, uint32_t* raw,
+                                         uint32_t* lsub, uint32_t* lbase, uint32_t* loff, uint32_t (*wred)[8],
+                                         uint32_t* wstage) {
+    constexpr int CT = RES_THREADS, IT = RES_IT, NW = CT / 64;
+    SelState* st = sel_region(head, q) + sd.slot;
+    const bool first = base == 0;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    /* ---- P0: the sample first, alone: the chunk loads would queue in front of it in memory */
+    WTP_RPROBE(0);
+    uint32_t ks[M_SAMPLE / CT];
+    sample_keys<CT, M_SAMPLE>(sd, ks);
+    if (first && tid == 0) { /* memory-side words: later adds come from other workgroups */
+        stc(reinterpret_cast<unsigned long long*>(&res[sd.res].zero_count), 0ull);
+        stc(&res[sd.res].path, 0);
+    }
+    /* the window BEFORE the chunk's loads: a wave cannot issue 24 KB of loads faster than its
+     * CU's share of HBM drains them, so code placed behind the issue waits for the stream */
+    WTP_RPROBE(8);
+    uint32_t kl, kh, sh;
+    if (WTP_RES_ABL & 1) { kl = 0x3c000000u + (ks[0] & 1u); kh = 0x3c800000u; sh = 13; }
+    else window_from_keys<CT, M_SAMPLE>(sd, ks, *reinterpret_cast<WindowLds<CT>*>(raw), &kl, &kh, &sh);
+    WTP_RPROBE(1);
+    float4 v[IT];
+    if (FULL) load_chunk<IT, CT>(sd.data + base, v);
+    else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
+    WTP_RPROBE(10);
+#ifdef WTP_RES_LOADWAIT
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    WTP_RPROBE(11);
+#endif
+    /* ---- P1: one branch-free pass over the registers: counters, and the keys inside (kl, kh]
+     * appended to the thread's own LDS column (slot j of thread t at col[j * CT]; every key is
+     * written to the next free slot and kept only if inside -- no branch, no atomic).  Slots
+     * past len were loaded as +0.0: never inside, and the block totals drop them once. */
+    const int nsub = 1 << sd.nsub_log2;
+    for (int i = tid; i < nsub; i += CT) lsub[i] = 0;
+    const uint32_t span = kh - kl; /* >= 1 */
+    uint32_t below = 0, eql = 0, mx = 0, cnt = 0;
+    uint32_t* col = wstage + tid;
+#pragma unroll
+    for (int it = 0; it < ((WTP_RES_ABL & 2) ? 1 : IT); ++it) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t k = abs_key(opaque(f4_get(v[it], c)));
+            const uint32_t d = k - kl; /* keys and kl < 2^31: bit 31 set iff k < kl */
+            mx = max(mx, k);
+            below += d >> 31;
+            eql += d == 0u;
+            col[min(cnt, (uint32_t)RES_STG) * CT] = k;
+            cnt += d - 1u < span;
+        }
+    }
+    {
+        const uint32_t r0 = wave_sum_u32(below), r1 = wave_sum_u32(eql), r2 = wave_max_u32(mx),
+                       r3 = wave_sum_u32(cnt), r4 = wave_max_u32(cnt);
+        if (lane == 0) { wred[wv][0] = r0; wred[wv][1] = r1; wred[wv][2] = r2; wred[wv][3] = r3; wred[wv][5] = r4; }
+    }
+    __syncthreads();
+    WTP_RPROBE(2);
+    uint32_t total = 0, wmax = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) { total += wred[w][3]; wmax = max(wmax, wred[w][5]); }
+    /* block-uniform: a thread's column or the block's sorted run overflowed -> the segment takes the full scan */
+    const bool ovf = wmax > (uint32_t)RES_STG || total > (uint32_t)RES_STAGE;
+    if (tid == 0) {
+        unsigned long long a0 = 0, a1 = 0;
+        uint32_t m2 = 0;
+        for (int w = 0; w < NW; ++w) { a0 += wred[w][0]; a1 += wred[w][1]; m2 = max(m2, wred[w][2]); }
+        const unsigned long long pad = (unsigned long long)(RES_CHUNK - len);
+        if (kl > 0) a0 -= pad; else a1 -= pad;
+        const int sh8 = blockIdx.x & (NSHARD - 1);
+        if (a0) atomicAdd(&st->below[sh8], a0);
+        if (a1) atomicAdd(&st->eq_lo[sh8], a1);
+        atomicMax(&st->maxkey[sh8], m2);
+        if (ovf) atomicOr(&st->overflow, 1u);
+    }
+    /* bucket the staged keys into this workgroup's own run (no reservation round trip): an LDS
+     * histogram, its exclusive scan (the run's bucket offsets), a counting sort in LDS, then the
+     * offsets and the sorted keys written through (sc1) as whole lines; the segment's bucket
+     * totals are no-return atomic adds */
+    uint32_t* run = cand + (int64_t)blockIdx.x * RES_WG_WORDS; /* [offsets: NSUB_MAX + 1][keys: RES_STAGE] */
+    if (!(WTP_RES_ABL & 4) && !ovf) { /* block-uniform */
+        for (uint32_t j0 = 0; j0 < cnt; j0 += 4) { /* four column reads in flight per step */
+            uint32_t kk[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) kk[q] = j0 + q < cnt ? col[(j0 + q) * CT] : 0u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (j0 + q < cnt) atomicAdd(&lsub[(kk[q] - kl - 1u) >> sh], 1u);
+        }
+        __syncthreads();
+        constexpr int PER = NSUB_MAX / CT; /* consecutive buckets per thread */
+        static_assert(PER * CT == NSUB_MAX, "bucket split");
+        const int per = (nsub + CT - 1) / CT;
+        uint32_t cj[PER];
+        uint32_t lsum = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int b = tid * per + j;
+            cj[j] = (j < per && b < nsub) ? lsub[b] : 0u;
+            lsum += cj[j];
+            if (cj[j]) atomicAdd(&st->sub[b], cj[j]);
+        }
+        const uint32_t incl = wave_scan_u32(lsum);
+        if (lane == 63) wred[wv][4] = incl;
+        __syncthreads();
+        uint32_t off = incl - lsum;
+        for (int w = 0; w < wv; ++w) off += wred[w][4];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int b = tid * per + j;
+            if (j < per && b < nsub) { loff[b] = off; stc(run + b, off); off += cj[j]; lsub[b] = 0; }
+        }
+        if (tid == 0) stc(run + nsub, total);
+        __syncthreads();
+        WTP_RPROBE(3);
+        uint32_t* sorted = raw; /* RES_STAGE keys; the window histogram is done with */
+        for (uint32_t j0 = 0; j0 < cnt; j0 += 4) { /* four reads, then four returning atomics, in flight */
+            uint32_t kk[4], at[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) kk[q] = j0 + q < cnt ? col[(j0 + q) * CT] : 0u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                at[q] = j0 + q < cnt ? atomicAdd(&lsub[(kk[q] - kl - 1u) >> sh], 1u) : 0u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (j0 + q < cnt) sorted[loff[(kk[q] - kl - 1u) >> sh] + at[q]] = kk[q];
+        }
+        __syncthreads();
+        WTP_RPROBE(16);
+        uint32_t* keys = run + RES_OFF_WORDS;
+        for (uint32_t i = tid; i < total; i += CT) stc(keys + i, sorted[i]);
+        WTP_RPROBE(17);
+    }
+    /* ---- grid barrier (arrive) */
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    WTP_RPROBE(4);
+    BarState* bar = bar_region(head, q);
+    if (tid == 0) atomicAdd(&bar->arrive[blockIdx.x & (NSHARD - 1)][0], 1u);
+    /* ---- speculative store while the other workgroups arrive: unless the window misses, every
+     * key < kl is below the threshold and every key > kh above it, so only keys in [kl, kh] are
+     * undecided -- write them unpruned now and fix the ones the threshold prunes after the
+     * select (in place, the input must stay intact for a possible full-scan select) */
+    float* qo = sd.out + base;
+    const bool spec = SPEC && sd.out != sd.data;
+    auto store_all = [&](auto&& g) {
+        if (FULL) {
+            float4* q4 = reinterpret_cast<float4*>(qo);
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                float4 y;
+                y.x = g(v[it].x); y.y = g(v[it].y); y.z = g(v[it].z); y.w = g(v[it].w);
+                q4[it * CT + tid] = y;
+            }
+        } else {
+            const __amdgpu_buffer_rsrc_t r = ragged_rsrc(qo, len);
+            const bool al = (sd.flags & SEG_ALIGNED) != 0;
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                float4 y;
+                y.x = g(v[it].x); y.y = g(v[it].y); y.z = g(v[it].z); y.w = g(v[it].w);
+                store4_tail(y, qo, r, it * CT + tid, len, al);
+            }
+        }
+    };
+    if (spec) store_all([&](float xv) { return abs_key(xv) < kl ? 0.0f : xv; });
+    WTP_RPROBE(9);
+    /* ---- grid barrier (wait) */
+    const int nblk = t.nblk;
+    bool ok = (WTP_RES_ABL & 16) ? true : res_wait(&bar->arrive[0][0], 32,
+                       [&](int s) { return (uint32_t)((nblk - s + NSHARD - 1) / NSHARD); }, NSHARD);
+    WTP_RPROBE(5);
+    if (blockIdx.x == 0 && tid == 0) head->parity = q ^ 1u; /* every workgroup has read it */
+    /* ---- P2 */
+    int path = 0;
+    const ResRuns rr{cand, sd.blk_begin, (int)((sd.n + RES_CHUNK - 1) / RES_CHUNK)};
+    const float thr = (WTP_RES_ABL & 8) ? __uint_as_float(kl)
+        : select_body<CT, true>(sd, st, cand, res, thr_out, raw, RES_STAGE, first, kl, kh, sh, &path, wstage, &rr);
+    WTP_RPROBE(6);
+    if (path == MODE_FULL && !spec) { /* in place: nobody writes before the segment's scans end */
+        __syncthreads();
+        if (tid == 0) atomicAdd(&st->seg_bar[0], 1ull);
+        const uint32_t nwg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
+        ok = res_wait(reinterpret_cast<const uint32_t*>(&st->seg_bar[0]), 0, [&](int) { return nwg; }, 1) && ok;
+    }
+    /* ---- P3: out = where(|x| < thr, 0, x) */
+    auto fin = [&](float xv) { return (fabsf(xv) < thr) ? 0.0f : xv; };
+    if (!spec || path == MODE_FULL || thr != thr) {
+        store_all(fin); /* uniform: everything (a NaN threshold prunes nothing) */
+    } else {
+        /* only the float4s holding a key in [kl, kh] that the threshold prunes */
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            bool fix = false;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float xv = f4_get(v[it], c);
+                fix = fix || (abs_key(xv) >= kl && fabsf(xv) < thr);
+            }
+            if (fix) {
+                float4 y;
+                y.x = fin(v[it].x); y.y = fin(v[it].y); y.z = fin(v[it].z); y.w = fin(v[it].w);
+                if (FULL) reinterpret_cast<float4*>(qo)[it * CT + tid] = y;
+                else store4_tail(y, qo, ragged_rsrc(qo, len), it * CT + tid, len, (sd.flags & SEG_ALIGNED) != 0);
+            }
+        }
+    }
+    if (thr != thr) { /* uniform: the copy's zeros are counted (the pad slots read as +0.0 excluded) */
+        uint32_t z = 0;
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) z += f4_get(v[it], c) == 0.0f;
+        const unsigned long long tot = block_sum_u64<CT>(z) - (unsigned long long)(RES_CHUNK - len);
+        if (tid == 0 && tot) atomicAdd((unsigned long long*)&res[sd.res].zero_count, tot);
+    }
+    if (!ok && tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+    WTP_RPROBE(7);
+}
+
+template <bool SPEC>
+__global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader* __restrict__ head,
+                                                          uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
+                                                          float* __restrict__ thr_out) {
+    constexpr size_t RAW = sizeof(WindowLds<RES_THREADS>) > RES_STAGE * 4 ? sizeof(WindowLds<RES_THREADS>) : RES_STAGE * 4;
+    __shared__ __attribute__((aligned(16))) uint32_t raw[RAW / 4]; /* P0 window histogram, then P2 stage */
+    __shared__ uint32_t lsub[NSUB_MAX], lbase[NSUB_MAX];
+    __shared__ uint32_t wred[RES_THREADS / 64][8];
+    __shared__ uint32_t loff[NSUB_MAX];
+    __shared__ uint32_t wstage[(RES_STG + 1) * RES_THREADS]; /* 66 KB: RES_STG slots + the discard slot per thread */
+    const uint32_t q = head->parity;
+    {   /* clear this workgroup's slice of the idle region (the previous launch's) */
+        uint4* idle = reinterpret_cast<uint4*>(sel_region(head, q ^ 1u));
+        constexpr int NV4 = (int)(SEL_REGION / 16);
+        const int per = (NV4 + (int)gridDim.x - 1) / (int)gridDim.x;
+        for (int i = threadIdx.x; i < per; i += RES_THREADS) {
+            const int j = (int)blockIdx.x * per + i;
+            if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    const int si = find_seg(t, blockIdx.x);
+    const SegDesc& sd = t.s[si];
+    const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * RES_CHUNK;
+    const int len = (int)min((int64_t)RES_CHUNK, sd.n - base);
+    if ((sd.flags & SEG_ALIGNED) && len == RES_CHUNK)
+        res_body<true, SPEC>(t, sd, head, q, cand, res, thr_out, base, len, raw, lsub, lbase, loff, wred, wstage);
+    else
+        res_body<false, SPEC>(t, sd, head, q, cand, res, thr_out, base, len, raw, lsub, lbase, loff, wred, wstage);
+}
+
+/* The in-place segments whose k_mask_select took the full-scan select: the mask pass that
+ * k_mask_select skipped for them, with the threshold it published (launched only for groups
+ * that hold an in-place level-0 segment; every other block returns at once). */
+__global__ __launch_bounds__(STREAM_THREADS) void k_mask_inplace(SegTable t, const wtp_result* __restrict__ res,
+                                                                 const float* __restrict__ thr_in) {
+    const int si = find_seg(t, blockIdx.x);
+    const SegDesc& sd = t.s[si];
+    if (!(sd.flags & SEG_MASK) || sd.data != sd.out || res[sd.res].path != MODE_FULL) return;
+    const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * CHUNK;
+    const int len = (int)min((int64_t)CHUNK, sd.n - base);
+    const float thr = thr_in[sd.res];
+    if ((sd.flags & SEG_ALIGNED) && len == CHUNK) (void)mask_body<true>(sd, base, len, thr);
+    else (void)mask_body<false>(sd, base, len, thr);
+}
+
 /* -------------------------------------------------------- min-weight pruning --- */
 /* percentage_min_pruning (ResNet/min_weight_pruning.py:66-74): zero the k smallest |w| of each
  * tensor.  The rank-(k-1) key t comes from the same window / collect / select machinery
@@ -787,7 +1350,7 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_minsel(SegTable t, const Sel
     const SelState* st = sel_region(const_cast<SelHeader*>(head), head->parity ^ 1u) + sd.slot;
     const int64_t k = (sd.flags & SEG_KZERO) ? 0 : sd.r0 + 1;
     float thr = 0.0f;
-    if (k > 0) thr = select_body<STREAM_THREADS>(sd, st, cand, res, thr_out, stage, 4096, true);
+    if (k > 0) thr = select_body<STREAM_THREADS>(sd, st, cand, res, thr_out, stage, 4096, true, st->kl, st->kh, st->shift);
     __syncthreads();
     if (threadIdx.x == 0) {
         wtp_result& r = res[sd.res];
@@ -1068,6 +1631,32 @@ void launch_minprune(const SegTable& t, SelHeader* head, const uint32_t* cand, w
 void launch_mask_select(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
                         hipStream_t s) {
     hipLaunchKernelGGL(k_mask_select, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, head, cand, res, thr_out);
+}
+void launch_mask_inplace(const SegTable& t, const wtp_result* res, const float* thr, hipStream_t s) {
+    hipLaunchKernelGGL(k_mask_inplace, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, res, thr);
+}
+int resident_capacity() {
+    static std::atomic<int> cache[16];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+    if (dev < 16) {
+        const int c = cache[dev].load(std::memory_order_relaxed);
+        if (c) return c > 0 ? c : 0;
+    }
+    int per = 0, cus = 0;
+    int cap = -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_resident<true>, RES_THREADS, 0) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && per >= 1 && cus > 0)
+        cap = cus; /* one workgroup per CU: the form the inter-workgroup hand-off is specified for */
+    (void)hipGetLastError();
+    if (dev < 16) cache[dev].store(cap, std::memory_order_relaxed);
+    return cap > 0 ? cap : 0;
+}
+void launch_resident(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
+                     hipStream_t s) {
+    static const int spec = [] { const char* e = getenv("WTP_RES_SPEC"); return e ? atoi(e) : 0; }();
+    if (spec) hipLaunchKernelGGL(k_resident<true>, dim3(t.nblk), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
+    else hipLaunchKernelGGL(k_resident<false>, dim3(t.nblk), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
 }
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
                      hipStream_t s) {

@@ -103,7 +103,7 @@ struct alignas(128) SelState {
     unsigned long long below[NSHARD]; /* atomicAdd (k_collect): keys < kl                    */
     unsigned long long eq_lo[NSHARD]; /* keys == kl                                          */
     unsigned long long eq_hi[NSHARD]; /* unused (keys == kh are bucketed with the inside keys) */
-    unsigned long long spare[NSHARD];
+    unsigned long long seg_bar[NSHARD]; /* k_resident: [0] = workgroups of the segment past a full-scan select */
     uint32_t maxkey[NSHARD];          /* atomicMax (k_collect)                               */
     uint32_t overflow;                /* a block had more inside keys than it can stage     */
     uint32_t pad0[23];
@@ -127,12 +127,21 @@ struct alignas(128) SelHeader {
     uint32_t done; /* k_collect blocks finished (last one flips parity and clears this) */
     uint32_t pad[30];
 };
-constexpr size_t SEL_REGION = SEG_PER_LAUNCH * sizeof(SelState);
+/* k_resident's grid barrier: one arrival counter per shard (blockIdx % 8, i.e. per XCD under
+ * the round-robin placement), each on its own 128-byte line; kept in the parity region so it is
+ * zero at the start of every launch that uses the region. */
+struct alignas(128) BarState {
+    uint32_t arrive[NSHARD][32];
+};
+constexpr size_t SEL_REGION = SEG_PER_LAUNCH * sizeof(SelState) + sizeof(BarState);
 __host__ __device__ inline SelState* sel_region(void* head, uint32_t q) {
     return reinterpret_cast<SelState*>(reinterpret_cast<char*>(head) + sizeof(SelHeader) + (size_t)q * SEL_REGION);
 }
+__host__ __device__ inline BarState* bar_region(void* head, uint32_t q) {
+    return reinterpret_cast<BarState*>(reinterpret_cast<char*>(sel_region(head, q)) + SEG_PER_LAUNCH * sizeof(SelState));
+}
 
-enum SelMode : int32_t { MODE_CAND = 1, MODE_WINDOW = 2, MODE_FULL = 3 };
+enum SelMode : int32_t { MODE_CAND = 1, MODE_WINDOW = 2, MODE_FULL = 3, MODE_FAULT = 99 };
 
 /* filter taps as a kernel argument (scalar-loaded, uniform across the wave) */
 struct Taps {
@@ -146,6 +155,25 @@ void launch_window(const SegTable& t, SelHeader* head, hipStream_t s);
 void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s);
 void launch_mask_select(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
                         hipStream_t s);
+/* after launch_mask_select: the in-place level-0 segments whose select fell back to the full scan */
+void launch_mask_inplace(const SegTable& t, const wtp_result* res, const float* thr, hipStream_t s);
+/* one-launch level-0 prune (k_resident): every segment SEG_MASK, blk_begin in RES_CHUNK units,
+ * t.nblk <= resident_capacity() */
+constexpr int RES_THREADS = 512;
+constexpr int RES_IT = 24;                          /* float4 per thread held in VGPRs */
+constexpr int RES_CHUNK = RES_THREADS * RES_IT * 4; /* 49152 elements per workgroup   */
+constexpr int RES_MAX_WG = 256;                     /* workgroups a resident launch may hold (<= CUs) */
+constexpr int RES_STAGE = 12288;                    /* inside keys a workgroup may keep (its sorted run) */
+constexpr int RES_OFF_WORDS = NSUB_MAX + 32;        /* a run's bucket offsets (+ total), padded to whole lines */
+constexpr int RES_WG_WORDS = RES_OFF_WORDS + RES_STAGE; /* one workgroup's run in the candidate region */
+/* the runs of one segment for the select: workgroups [wb, wb + nw) of the launch */
+struct ResRuns {
+    const uint32_t* base;
+    int wb, nw;
+};
+int resident_capacity();                            /* co-resident workgroups on the current device */
+void launch_resident(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
+                     hipStream_t s);
 /* min-weight pruning after window + collect: mp = 16 B per tensor, tiecnt = one u32 per
  * streaming block */
 void launch_minprune(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,

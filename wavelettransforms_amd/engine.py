@@ -119,9 +119,15 @@ def launch(tensors, wavelet, level, pct, outs=None, carry_level=True, stream=Non
     return outs, res
 
 
+MODE_FAULT = 99  # k_resident's grid was not co-resident: its barrier timed out (include/wtprune.h)
+
+
 def decode(results_dev, n):
     host = results_dev.cpu().numpy().view(RESULT_DTYPE)[:n]
     out = []
+    if (host["path"] == MODE_FAULT).any():
+        raise RuntimeError("wavelettransforms_amd: the resident launch could not hold its whole grid on the GPU "
+                           "(other kernels occupied CUs); results are invalid -- call set_resident(False)")
     for r in host:
         d = {k: r[k].item() for k in RESULT_DTYPE.names}
         d["thr32"] = float(np.array(d["thr32_bits"], np.uint32).view(np.float32))
@@ -129,6 +135,16 @@ def decode(results_dev, n):
         d["nonzero"] = d["numel"] - d["zero_count"]
         out.append(d)
     return out
+
+
+def set_resident(enabled):
+    """Allow (default) or forbid the one-launch resident form of level-0 groups; returns the previous setting."""
+    return bool(N.lib().wtp_set_resident(1 if enabled else 0))
+
+
+def resident_capacity():
+    """Workgroups (of 49152 weights) the resident launch can hold on the current device; 0: never used."""
+    return int(N.lib().wtp_resident_capacity())
 
 
 def prune(tensors, wavelet, level, pct, outs=None, carry_level=True):
