@@ -298,6 +298,67 @@ __device__ __forceinline__ void window_from_keys(const SegDesc& sd, const uint32
 }
 
 
+/* window_from_keys for ONE wave (64 threads, no block barrier: the other waves of the block
+ * are elsewhere).  Lane l owns the FBP consecutive bins from l * FBP (stride FBP odd: no bank
+ * conflicts); the lane whose run holds a sample rank walks it. */
+/* The search half of window_from_keys for ONE wave (no block barrier: the other waves are
+ * issuing their loads meanwhile), over the block's histogram h of the MS sampled keys (NB bins)
+ * and its coarse companion hc (bins of 128: WCB of them): one scan over the coarse bins finds
+ * the 128 fine bins holding a sample rank, one more scan over those finds the bin. */
+constexpr int WCB = (NB + 127) / 128; /* 33 <= 64 */
+__device__ __forceinline__ int wave_find_bin(const uint32_t* h, const uint32_t* hc, int r) {
+    const int lane = threadIdx.x & 63;
+    if (r < 0) return -1;
+    const uint32_t c = lane < WCB ? hc[lane] : 0u;
+    const uint32_t incl = wave_scan_u32(c);
+    const uint64_t m = __ballot((int)(incl - c) <= r && r < (int)incl);
+    if (!m) return -1;
+    const int cb = __ffsll((unsigned long long)m) - 1;
+    const int before = __builtin_amdgcn_readlane((int)(incl - c), cb);
+    const int b0 = cb * 128 + 2 * lane;
+    const uint32_t f0 = b0 < NB ? h[b0] : 0u, f1 = b0 + 1 < NB ? h[b0 + 1] : 0u;
+    const uint32_t s2 = f0 + f1;
+    const int i2 = before + (int)wave_scan_u32(s2);
+    const int e2 = i2 - (int)s2;
+    const uint64_t m2 = __ballot(e2 <= r && r < i2);
+    const int L = __ffsll((unsigned long long)m2) - 1;
+    const int pick = (r < e2 + (int)f0) ? b0 : b0 + 1;
+    return __builtin_amdgcn_readlane(pick, L);
+}
+
+template <int MS>
+__device__ __forceinline__ void window_search_wave(const SegDesc& sd, const uint32_t* h, const uint32_t* hc,
+                                                   uint32_t* kl_out, uint32_t* kh_out, uint32_t* sh_out) {
+    const int64_t n = sd.n;
+    const bool exact = n <= MS;
+    const int m = exact ? (int)n : MS;
+    const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
+    int sa, sb;
+    if (exact) {
+        sa = (int)r0;
+        sb = (int)r1;
+    } else {
+        const double p = (double)r0 / (double)(n - 1);
+        const double s0 = p * (double)(m - 1), s1 = (double)r1 / (double)(n - 1) * (double)(m - 1);
+        const double d = 6.0 * sqrt((double)m * p * (1.0 - p)) + 24.0;
+        sa = (int)floor(s0 - d);
+        sb = (int)ceil(s1 + d);
+    }
+    const int f0 = wave_find_bin(h, hc, sa);
+    const int f1 = sb < m ? wave_find_bin(h, hc, sb) : -1;
+    const uint32_t kl = (sa < 0 || f0 < 0) ? 0u : bin_lo_key(f0);
+    const uint32_t kh = (sb >= m || f1 < 0) ? 0xFFFFFFFFu : bin_hi_key(f1);
+    uint32_t sh = 0;
+    if (kh > kl + 1) {
+        const uint32_t R = kh - kl - 1;
+        const int bits = 32 - __clz(R);
+        sh = bits > sd.nsub_log2 ? bits - sd.nsub_log2 : 0;
+    }
+    *kl_out = kl;
+    *kh_out = kh;
+    *sh_out = sh;
+}
+
 /* -------------------------------------------------------------- k_collect --- */
 /* LAB: 0 = the production kernel; 1 = stop after the counters; 2 = stop after the bucket
  * histogram (tools/mb/lab.hip ablations).  IT float4 per thread: a sub-chunk of IT * CT * 4
@@ -1066,30 +1127,45 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     SelState* st = sel_region(head, q) + sd.slot;
     const bool first = base == 0;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    /* ---- P0: the sample first, alone: the chunk loads would queue in front of it in memory */
+    /* ---- P0: every thread loads its share of the sample and adds it to the LDS histogram;
+     * then wave 0 searches the histogram for the window while waves 1.. issue the chunk's loads
+     * (a wave stalls while its own 24 loads issue, so the search needs a wave of its own).  The
+     * sample loads go out before any chunk load, ahead of the stream in the memory queues. */
     WTP_RPROBE(0);
-    uint32_t ks[M_SAMPLE / CT];
-    sample_keys<CT, M_SAMPLE>(sd, ks);
-    if (first && tid == 0) { /* memory-side words: later adds come from other workgroups */
-        stc(reinterpret_cast<unsigned long long*>(&res[sd.res].zero_count), 0ull);
-        stc(&res[sd.res].path, 0);
-    }
-    /* the window BEFORE the chunk's loads: a wave cannot issue 24 KB of loads faster than its
-     * CU's share of HBM drains them, so code placed behind the issue waits for the stream */
-    WTP_RPROBE(8);
-    uint32_t kl, kh, sh;
-    if (WTP_RES_ABL & 1) { kl = 0x3c000000u + (ks[0] & 1u); kh = 0x3c800000u; sh = 13; }
-    else window_from_keys<CT, M_SAMPLE>(sd, ks, *reinterpret_cast<WindowLds<CT>*>(raw), &kl, &kh, &sh);
-    WTP_RPROBE(1);
+    __shared__ uint32_t s_win[3];
     float4 v[IT];
+    {
+        uint32_t ks[M_SAMPLE / CT];
+        sample_keys<CT, M_SAMPLE>(sd, ks);
+        for (int j = tid; j < NB + WCB; j += CT) raw[j] = 0u; /* fine bins, then the coarse bins */
+        if (first && tid == 0) { /* memory-side words: later adds come from other workgroups */
+            stc(reinterpret_cast<unsigned long long*>(&res[sd.res].zero_count), 0ull);
+            stc(&res[sd.res].path, 0);
+        }
+        const int m = sd.n <= M_SAMPLE ? (int)sd.n : M_SAMPLE;
+        __syncthreads();
+        WTP_RPROBE(8);
+#pragma unroll
+        for (int j = 0; j < M_SAMPLE / CT; ++j)
+            if (j * CT + tid < m) {
+                const int b = key_bin(ks[j]);
+                atomicAdd(&raw[b], 1u);
+                atomicAdd(&raw[NB + (b >> 7)], 1u);
+            }
+        __syncthreads();
+    }
+    if (wv == 0) {
+        uint32_t wkl, wkh, wsh;
+        if (WTP_RES_ABL & 1) { wkl = 0x3c000000u; wkh = 0x3c800000u; wsh = 13; }
+        else window_search_wave<M_SAMPLE>(sd, raw, raw + NB, &wkl, &wkh, &wsh);
+        if (lane == 0) { s_win[0] = wkl; s_win[1] = wkh; s_win[2] = wsh; }
+        WTP_RPROBE(1);
+    }
     if (FULL) load_chunk<IT, CT>(sd.data + base, v);
     else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
     WTP_RPROBE(10);
-#ifdef WTP_RES_LOADWAIT
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    WTP_RPROBE(11);
-#endif
+    const uint32_t kl = s_win[0], kh = s_win[1], sh = s_win[2];
     /* ---- P1: one branch-free pass over the registers: counters, and the keys inside (kl, kh]
      * appended to the thread's own LDS column (slot j of thread t at col[j * CT]; every key is
      * written to the next free slot and kept only if inside -- no branch, no atomic).  Slots
