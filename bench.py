@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cold", action="store_true", help="also time with the Infinity Cache flushed")
+    ap.add_argument("--flatten", action="store_true",
+                    help="the 1-D flattened mode (WTP_FLATTEN; an extension, not the headline path)")
     ap.add_argument("--no-resident", action="store_true",
                     help="level-0 groups in the three-launch form instead of the one-launch k_resident")
     return ap.parse_args()
@@ -103,7 +105,7 @@ def main():
     n_w = sum(x.numel() for x in xs)
 
     def step():
-        return engine.launch(xs, wavelet, level, pct, outs=outs, carry_level=False)
+        return engine.launch(xs, wavelet, level, pct, outs=outs, carry_level=False, flatten=args.flatten)
 
     for _ in range(max(1, args.warmup)):
         _, res = step()
@@ -257,7 +259,8 @@ def main():
             "config": {"workload": name, "config": args.config, "wavelet": wavelet, "level": level,
                        "percentile": pct, "weights_per_gpu_step": n_w, "coeffs_per_gpu_step": pop,
                        "tensors": len(xs), "eff_levels": sorted({r["eff_level"] for r in recs}),
-                       "graph_steps": G if graph is not None else 0, "parallelism": "replica%d" % world},
+                       "graph_steps": G if graph is not None else 0, "parallelism": "replica%d" % world,
+                       "transform": "1-D flattened (extension)" if args.flatten else "2-D over (kh, kw) (reference)"},
             "pipeline_hbm_gbs": 8 * n_w * K / T / 1e9,
             "roofline": {"bound": "hbm", "kernel": kernel_of.get(dom, dom), "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

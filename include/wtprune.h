@@ -99,6 +99,20 @@ int wtp_prune_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int l
 int wtp_prune_layers_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct,
                          void* workspace, size_t workspace_bytes, wtp_result* results_dev, wtp_stream_t stream);
 
+/* The general entry: flags = WTP_CARRY_LEVEL (wtp_prune_f32's level carry) | WTP_FLATTEN.
+ * WTP_FLATTEN is the 1-D flattened mode (an extension: the reference's transform is 2-D): every
+ * tensor with ndim >= 2 is transformed as ONE line, pywt.wavedec(w.ravel(), wavelet,
+ * 'periodization', level) with the level clamped to pywt.dwt_max_level(numel, dec_len) (carried
+ * over the list under WTP_CARRY_LEVEL), packed by pywt.coeffs_to_array ([cA_L | cD_L | ... |
+ * cD_1]), thresholded at the pct-th percentile of |coeffs| exactly as the 2-D path, rebuilt by
+ * pywt.waverec and cut to numel; ndim < 2 tensors keep the plain-percentile branch (:58-62).
+ * Workspace: wtp_workspace_size_ex with the same flags. */
+#define WTP_CARRY_LEVEL 1
+#define WTP_FLATTEN 2
+size_t wtp_workspace_size_ex(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, int flags);
+int wtp_prune_ex_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, int flags,
+                     void* workspace, size_t workspace_bytes, wtp_result* results_dev, wtp_stream_t stream);
+
 /* percentile_based_thresholding(arr, pct) on n device floats: out = where(|in| < thr, 0, in) */
 int wtp_threshold_f32(const float* in, float* out, int64_t n, double pct, void* workspace,
                       size_t workspace_bytes, wtp_result* result_dev, wtp_stream_t stream);

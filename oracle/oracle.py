@@ -76,6 +76,7 @@ def lib():
                                               P(ctypes.c_double), f32p]
         L.or_prune_tensor.argtypes = [f32p, f32p, ctypes.c_int, i64p, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_double, P(OrResult), f32p]
+        L.or_prune_tensor_flat.argtypes = L.or_prune_tensor.argtypes
         L.or_prune_batch.argtypes = [ctypes.c_int, P(f32p), P(f32p), P(ctypes.c_int), i64p,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_double, P(OrResult),
                                      ctypes.c_int]
@@ -201,6 +202,34 @@ def prune_tensor(x, wavelet, level, pct, want_coeffs=False):
         cptr = _f32p(coeffs.reshape(-1))
     rc = lib().or_prune_tensor(_f32p(x.reshape(-1)) if x.size else None, _f32p(out.reshape(-1)) if x.size else None,
                                x.ndim, shape, wid, int(level), float(pct), ctypes.byref(res), cptr)
+    _check(rc, wavelet)
+    d = res.as_dict()
+    return (out, d, coeffs) if want_coeffs else (out, d)
+
+
+def prune_tensor_flat(x, wavelet, level, pct, want_coeffs=False):
+    """The 1-D flattened mode (WTP_FLATTEN, include/wtprune.h): ndim >= 2 tensors through
+    pywt.wavedec / coeffs_to_array / percentile threshold / waverec of w.ravel(); ndim < 2 as
+    prune_tensor.  Returns (out, result dict[, packed coeffs])."""
+    x = np.require(np.asarray(x, np.float32), requirements="C")
+    if x.ndim < 2:
+        return prune_tensor(x, wavelet, level, pct, want_coeffs)
+    out = np.empty_like(x)
+    shape = (ctypes.c_int64 * x.ndim)(*x.shape)
+    res = OrResult()
+    wid = wavelet_id(wavelet)
+    coeffs, cptr = None, None
+    if want_coeffs:
+        n = x.size
+        L = max(0, min(level, dwt_max_level(n, lib().or_dec_len(wid)))) if wid >= 0 else 0
+        lens = [n]
+        for _ in range(L):
+            lens.append((lens[-1] + 1) // 2)
+        coeffs = np.empty(lens[-1] + sum(lens[1:]), np.float32)
+        cptr = _f32p(coeffs)
+    rc = lib().or_prune_tensor_flat(_f32p(x.reshape(-1)) if x.size else None,
+                                    _f32p(out.reshape(-1)) if x.size else None, x.ndim, shape, wid, int(level),
+                                    float(pct), ctypes.byref(res), cptr)
     _check(rc, wavelet)
     d = res.as_dict()
     return (out, d, coeffs) if want_coeffs else (out, d)

@@ -459,6 +459,75 @@ int or_prune_tensor(const float* in, float* out, int ndim, const int64_t* shape,
     return res->status = OR_OK;
 }
 
+/* 1-D flattened mode (WTP_FLATTEN; an extension -- the reference transform is 2-D): tensors
+ * with ndim >= 2 go through pywt.wavedec(w.ravel(), wavelet, 'periodization', L) with L =
+ * min(level, dwt_max_level(numel, dec_len)) (pywt/_multilevel.py wavedec), coeffs_to_array
+ * ([cA_L | cD_L | ... | cD_1]), the same percentile threshold as :25-32, array_to_coeffs,
+ * waverec (its crop of a to len(d) when one longer, pywt/_multilevel.py waverec) and the cut
+ * to numel; ndim < 2 keeps the plain-percentile branch (:58-62). */
+int or_prune_tensor_flat(const float* in, float* out, int ndim, const int64_t* shape, int wid, int level,
+                         double pct, or_result* res, float* coeff_out) {
+    if (ndim < 2) return or_prune_tensor(in, out, ndim, shape, wid, level, pct, res, coeff_out);
+    memset(res, 0, sizeof(*res));
+    int64_t N = 1;
+    for (int i = 0; i < ndim; ++i) N *= shape[i];
+    res->numel = N;
+    if (wid < 0 || wid >= WT_NUM_WAVELETS) return res->status = OR_EBADWAVELET;
+    const int maxL = or_dwt_max_level(N, wt_flen[wid]);
+    const int L = level < maxL ? level : maxL;
+    res->eff_level = L;
+    if (L < 0) return res->status = OR_EBADLEVEL;
+    int64_t len[34];
+    len[0] = N;
+    for (int k = 1; k <= L; ++k) len[k] = (len[k - 1] + 1) / 2;
+    int64_t pop = len[L];
+    for (int k = 1; k <= L; ++k) pop += len[k];
+    res->coeff_numel = pop;
+    res->packed_rows = 1;
+    res->packed_cols = pop;
+    if (pop == 0) return res->status = OR_EEMPTY;
+    float* P = (float*)malloc(sizeof(float) * (size_t)pop);
+    float* A = (float*)malloc(sizeof(float) * (size_t)(N + 2));
+    float* B = (float*)malloc(sizeof(float) * (size_t)(N + 2));
+    if (!P || !A || !B) { free(P); free(A); free(B); return res->status = OR_ENOMEM; }
+    /* wavedec: level k turns a_{k-1} (len[k-1]) into a_k, d_k; d_k lands at its packed offset */
+    memcpy(A, in, sizeof(float) * (size_t)N);
+    int64_t off = pop;
+    for (int k = 1; k <= L; ++k) {
+        off -= len[k]; /* cD_1 is last, cD_L right after cA_L */
+        dwt1(A, 1, len[k - 1], wid, B, P + off, 1);
+        float* t = A; A = B; B = t;
+    }
+    memcpy(P, A, sizeof(float) * (size_t)len[L]);
+    if (coeff_out) memcpy(coeff_out, P, sizeof(float) * (size_t)pop);
+    int rc = or_percentile_abs(P, pop, pct, &res->thr64, &res->max_abs);
+    if (rc == OR_OK) {
+        const float thr32 = (float)res->thr64;
+        for (int64_t i = 0; i < pop; ++i) P[i] = thr_load(P[i], 1, thr32);
+        if (L == 0) {
+            memcpy(out, P, sizeof(float) * (size_t)N);
+        } else {
+            /* waverec: a starts as the packed cA_L; idwt(a[:len(d)], d) per level */
+            memcpy(A, P, sizeof(float) * (size_t)len[L]);
+            int64_t doff = len[L];
+            for (int k = L; k >= 1; --k) {
+                idwt1(A, P + doff, 1, len[k], wid, B, 1); /* 2 len[k] samples; A holds >= len[k] */
+                doff += len[k];
+                float* t = A; A = B; B = t;
+            }
+            memcpy(out, A, sizeof(float) * (size_t)N);
+        }
+    }
+    free(P); free(A); free(B);
+    if (rc != OR_OK) return res->status = rc;
+    res->thr32 = (float)res->thr64;
+    int64_t z = 0;
+    for (int64_t i = 0; i < N; ++i) z += (out[i] == 0.0f);
+    res->zero_count = z;
+    res->nonzero = N - z;
+    return res->status = OR_OK;
+}
+
 /* A batch of independent tensors (one pruning "step" of the CPU baseline), threaded over
  * tensors with OpenMP when nthreads > 1 (the reference loop is sequential: 1 thread). */
 int or_prune_batch(int ntensors, const float* const* ins, float* const* outs, const int* ndims,

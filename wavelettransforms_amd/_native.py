@@ -67,6 +67,8 @@ def lib():
             "wtp_workspace_init": ([vp, sz, vp], i32),
             "wtp_prune_f32": ([tp, i32, i32, i32, f64, vp, sz, vp, vp], i32),
             "wtp_prune_layers_f32": ([tp, i32, i32, i32, f64, vp, sz, vp, vp], i32),
+            "wtp_workspace_size_ex": ([tp, i32, i32, i32, i32], sz),
+            "wtp_prune_ex_f32": ([tp, i32, i32, i32, f64, i32, vp, sz, vp, vp], i32),
             "wtp_threshold_f32": ([vp, vp, i64, f64, vp, sz, vp, vp], i32),
             "wtp_dwt_workspace_size": ([i64, i64, i64, i32], sz),
             "wtp_wavedec2_f32": ([vp, vp, i64, i64, i64, i32, i32, vp, sz, vp], i32),

@@ -81,6 +81,8 @@ struct TPlan {
     size_t cand_off = 0;  /* element offset into the candidate region                   */
     size_t t_off = 0;     /* workspace byte offset of this tensor's three level temps      */
     size_t t_elems = 0;   /* elements per temp                                              */
+    bool flat = false;    /* 1-D flattened mode: pywt.wavedec / waverec of the flat tensor   */
+    int64_t len[34] = {}; /* flat: len[0] = numel, len[k] = ceil(len[k-1] / 2)              */
 };
 
 struct Layout {
@@ -116,7 +118,7 @@ int64_t cap_for(int64_t n) {
 
 /* Validate and plan every tensor in the reference's order; returns WTP_OK or the first error. */
 int plan_tensors(const wtp_tensor* ts, int n, int wid, int level, double pct, bool check_ptrs,
-                 std::vector<TPlan>& out, bool carry = true) {
+                 std::vector<TPlan>& out, bool carry = true, bool flat = false) {
     out.assign(n, TPlan());
     int cur_level = level;
     for (int t = 0; t < n; ++t) {
@@ -137,6 +139,24 @@ int plan_tensors(const wtp_tensor* ts, int n, int wid, int level, double pct, bo
             if (p.numel == 0) return fail(WTP_EEMPTY, t, "index -1 is out of bounds for axis 0 with size 0");
             p.L = cur_level;
             p.pop = p.numel;
+        } else if (flat) {
+            /* 1-D flattened mode: pywt.wavedec(w.ravel(), wavelet, 'periodization', level) with
+             * the level clamped as calculate_max_level clamps it for the 2-D path (:12-13, :64-65) */
+            if (wid < 0 || wid >= WT_NUM_WAVELETS)
+                return fail(WTP_EBADWAVELET, t, "Unknown wavelet name, check wavelist() for the list of available builtin wavelets.");
+            p.flat = true;
+            const int maxL = max_level(p.numel, wt_flen[wid]);
+            if (maxL < cur_level) cur_level = maxL;
+            p.L = cur_level;
+            if (p.L < 0) return fail(WTP_EBADLEVEL, t, "Level value of %d is too low . Minimum level is 0.", p.L);
+            if (p.L > 32) return fail(WTP_EARG, t, "tensor %d: level %d unsupported", t, p.L);
+            if (!pct_ok(pct)) return fail(WTP_EBADPCT, t, "Percentiles must be in the range [0, 100]");
+            p.len[0] = p.numel;
+            for (int k = 1; k <= p.L; ++k) p.len[k] = (p.len[k - 1] + 1) / 2;
+            p.pop = p.len[p.L];
+            for (int k = 1; k <= p.L; ++k) p.pop += p.len[k];
+            if (p.pop == 0) return fail(WTP_EEMPTY, t, "index -1 is out of bounds for axis 0 with size 0");
+            p.dwt = p.L > 0;
         } else {
             if (wid < 0 || wid >= WT_NUM_WAVELETS)
                 return fail(WTP_EBADWAVELET, t, "Unknown wavelet name, check wavelist() for the list of available builtin wavelets.");
@@ -200,6 +220,12 @@ Layout make_layout(std::vector<TPlan>& ps) {
      * launch, so their intermediate approximations are live together */
     for (auto& p : ps) {
         if (!p.dwt) continue;
+        if (p.flat) { /* two ping-pong lines of up to numel + 1 samples (the last synthesis output) */
+            p.t_elems = (size_t)p.numel + 2;
+            p.t_off = off;
+            off = align_up(off + 3 * align_up(p.t_elems * sizeof(float)));
+            continue;
+        }
         const int64_t r1 = p.g.R[1], c1 = p.g.C[1];
         const size_t a = (size_t)(p.B * r1 * (p.W > 2 * c1 ? p.W : 2 * c1));
         const size_t b = (size_t)(p.B * 2 * r1 * 2 * c1);
@@ -323,6 +349,39 @@ void inverse_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s)
     }
 }
 
+/* pywt.wavedec / waverec (periodization) of one flattened tensor (1-D mode): packed layout
+ * [cA_L | cD_L | cD_L-1 | ... | cD_1] (pywt.coeffs_to_array of a 1-D list) */
+int64_t flat_off_d(const TPlan& p, int k) {
+    int64_t off = p.len[p.L];
+    for (int j = p.L; j > k; --j) off += p.len[j];
+    return off;
+}
+
+void forward_flat(const TPlan& p, const float* in, float* P, float* T0, float* T1, const Taps& tp, hipStream_t s) {
+    const float* cur = in;
+    for (int k = 1; k <= p.L; ++k) {
+        float* a = (k == p.L) ? P : ((cur == T0) ? T1 : T0);
+        launch_dwt1_level(cur, p.len[k - 1], tp, a, P + flat_off_d(p, k), s);
+        cur = a;
+    }
+}
+
+/* each level reads a (the packed cA at the top, thresholded on load; then the previous level's
+ * output, of which the first len[k] samples are used -- waverec's crop) and the packed cD_k */
+void inverse_flat(const TPlan& p, const float* P, float* out, float* T0, float* T1, const Taps& tp, const float* thr,
+                  unsigned long long* zc, hipStream_t s) {
+    const float* a = P;
+    int a_thr = 1;
+    for (int k = p.L; k >= 1; --k) {
+        const bool final = k == 1;
+        float* y = final ? out : ((a == T0) ? T1 : T0);
+        launch_idwt1_level(a, a_thr, P + flat_off_d(p, k), p.len[k], tp, thr, y, final ? p.len[0] : 2 * p.len[k],
+                           final ? zc : nullptr, s);
+        a = y;
+        a_thr = 0;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -378,13 +437,13 @@ int wtp_workspace_init(void* ws, size_t bytes, wtp_stream_t stream) {
 }
 
 static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, void* ws,
-                      size_t ws_bytes, wtp_result* results, wtp_stream_t stream, bool carry) {
+                      size_t ws_bytes, wtp_result* results, wtp_stream_t stream, bool carry, bool flat = false) {
     g_err.clear();
     g_err_tensor = -1;
     if (ntensors < 0 || (ntensors > 0 && (!tensors || !results))) return fail(WTP_EARG, -1, "bad arguments");
     if (ntensors == 0) return WTP_OK;
     std::vector<TPlan> ps;
-    int rc = plan_tensors(tensors, ntensors, wavelet_id, level, pct, true, ps, carry);
+    int rc = plan_tensors(tensors, ntensors, wavelet_id, level, pct, true, ps, carry, flat);
     if (rc != WTP_OK) return rc;
     Layout lay = make_layout(ps);
     if (!ws || ws_bytes < lay.total)
@@ -401,6 +460,12 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     for (int t = 0; t < ntensors; ++t) {
         const TPlan& p = ps[t];
         if (!p.dwt) continue;
+        if (p.flat) {
+            float* T = reinterpret_cast<float*>(wsb(ws, p.t_off));
+            forward_flat(p, tensors[t].in, reinterpret_cast<float*>(wsb(ws, p.p_off)), T,
+                         T + align_up(p.t_elems * sizeof(float)) / sizeof(float), tp, s);
+            continue;
+        }
         Chain c;
         c.p = &p;
         c.in = tensors[t].in;
@@ -475,6 +540,14 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     }
     /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2) */
     inverse_chains(chains, tp, s);
+    for (int t = 0; t < ntensors; ++t) {
+        const TPlan& p = ps[t];
+        if (!p.flat || !p.dwt) continue;
+        float* T = reinterpret_cast<float*>(wsb(ws, p.t_off));
+        inverse_flat(p, reinterpret_cast<const float*>(wsb(ws, p.p_off)), tensors[t].out, T,
+                     T + align_up(p.t_elems * sizeof(float)) / sizeof(float), tp, thr_t + t,
+                     reinterpret_cast<unsigned long long*>(&results[t].zero_count), s);
+    }
     stage(5, s);
     return check_launch();
 }
@@ -487,6 +560,22 @@ int wtp_prune_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int l
 int wtp_prune_layers_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, void* ws,
                          size_t ws_bytes, wtp_result* results, wtp_stream_t stream) {
     return prune_impl(tensors, ntensors, wavelet_id, level, pct, ws, ws_bytes, results, stream, false);
+}
+
+size_t wtp_workspace_size_ex(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, int flags) {
+    if (ntensors < 0 || (ntensors > 0 && !tensors) || (flags & ~(WTP_CARRY_LEVEL | WTP_FLATTEN))) return 0;
+    std::vector<TPlan> ps;
+    if (plan_tensors(tensors, ntensors, wavelet_id, level, 50.0, false, ps, (flags & WTP_CARRY_LEVEL) != 0,
+                     (flags & WTP_FLATTEN) != 0) != WTP_OK)
+        return 0;
+    return make_layout(ps).total;
+}
+
+int wtp_prune_ex_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, int flags,
+                     void* ws, size_t ws_bytes, wtp_result* results, wtp_stream_t stream) {
+    if (flags & ~(WTP_CARRY_LEVEL | WTP_FLATTEN)) return fail(WTP_EARG, -1, "bad flags 0x%x", flags);
+    return prune_impl(tensors, ntensors, wavelet_id, level, pct, ws, ws_bytes, results, stream,
+                      (flags & WTP_CARRY_LEVEL) != 0, (flags & WTP_FLATTEN) != 0);
 }
 
 /* ---------------------------------------------------------- min pruning --- */

@@ -1657,6 +1657,44 @@ __global__ __launch_bounds__(DWT_THREADS) void k_idwt_cols(const float* __restri
     }
 }
 
+/* ---- 1-D flattened mode: pywt.wavedec / waverec (periodization) of the flattened tensor ----
+ * k_dwt1_level: one analysis level of a line of N samples -> a (ceil(N/2)) and d (ceil(N/2)),
+ * one thread per output pair, summed in PyWavelets' order (wt_ana_point). */
+__global__ __launch_bounds__(DWT_THREADS) void k_dwt1_level(const float* __restrict__ x, int64_t N, Taps tp,
+                                                            float* __restrict__ a, float* __restrict__ d) {
+    const int64_t M = (N + 1) / 2;
+    for (int64_t o = (int64_t)blockIdx.x * DWT_THREADS + threadIdx.x; o < M; o += (int64_t)gridDim.x * DWT_THREADS) {
+        float sa, sd;
+        wt_ana_point(o, N, tp.F, tp.f[0], tp.f[1], [&](int64_t k) { return x[k]; }, sa, sd);
+        a[o] = sa;
+        d[o] = sd;
+    }
+}
+
+/* One synthesis level (pywt.waverec's loop body): a cropped to len(d) = N when it is one longer,
+ * idwt(a, d) -> 2N outputs, of which the first outN are written.  a_thr: threshold a on load
+ * (the packed cA of the top level); d is always a packed detail band (thresholded on load).
+ * thr == nullptr: no threshold.  The last level crops to the tensor and counts its zeros. */
+__global__ __launch_bounds__(DWT_THREADS) void k_idwt1_level(const float* __restrict__ a, int a_thr,
+                                                             const float* __restrict__ d, int64_t N, Taps tp,
+                                                             const float* __restrict__ thr, float* __restrict__ y,
+                                                             int64_t outN, unsigned long long* zero_count) {
+    const float t = thr ? *thr : 0.0f;
+    const bool ta = thr && a_thr, td = thr != nullptr;
+    unsigned long long z = 0;
+    for (int64_t n = (int64_t)blockIdx.x * DWT_THREADS + threadIdx.x; n < outN; n += (int64_t)gridDim.x * DWT_THREADS) {
+        const float v = wt_syn_point(n, N, tp.F, tp.f[2], tp.f[3],
+                                     [&](int64_t k) { return ta ? thr_load(a[k], t) : a[k]; },
+                                     [&](int64_t k) { return td ? thr_load(d[k], t) : d[k]; });
+        y[n] = v;
+        z += (v == 0.0f);
+    }
+    if (zero_count) {
+        const unsigned long long tot = block_sum_u64<DWT_THREADS>(z);
+        if (threadIdx.x == 0 && tot) atomicAdd(zero_count, tot);
+    }
+}
+
 __global__ __launch_bounds__(DWT_THREADS) void k_copy_threshold(const float* __restrict__ P, float* __restrict__ out,
                                                                 int64_t n, const float* thrp,
                                                                 unsigned long long* zero_count) {
@@ -1754,6 +1792,14 @@ void launch_idwt_cols(const float* lo, const float* hi, int64_t B, int64_t R, in
                       int64_t outH, int64_t outW, unsigned long long* zero_count, hipStream_t s) {
     hipLaunchKernelGGL(k_idwt_cols, dim3(grid_for(B * outH * outW)), dim3(DWT_THREADS), 0, s, lo, hi, B, R, 2 * C, tp,
                        y, outH, outW, zero_count);
+}
+void launch_dwt1_level(const float* x, int64_t N, const Taps& tp, float* a, float* d, hipStream_t s) {
+    hipLaunchKernelGGL(k_dwt1_level, dim3(grid_for((N + 1) / 2)), dim3(DWT_THREADS), 0, s, x, N, tp, a, d);
+}
+void launch_idwt1_level(const float* a, int a_thr, const float* d, int64_t N, const Taps& tp, const float* thr,
+                        float* y, int64_t outN, unsigned long long* zc, hipStream_t s) {
+    hipLaunchKernelGGL(k_idwt1_level, dim3(grid_for(outN)), dim3(DWT_THREADS), 0, s, a, a_thr, d, N, tp, thr, y, outN,
+                       zc);
 }
 void launch_copy_threshold(const float* P, float* out, int64_t n, const float* thr, unsigned long long* zc,
                            hipStream_t s) {

@@ -220,6 +220,10 @@ void launch_inv_level(const float* a_src, int64_t a_bs, int64_t lda, int a_from_
                       hipStream_t s);
 void launch_copy_threshold(const float* P, float* out, int64_t n, const float* thr, unsigned long long* zc,
                            hipStream_t s);
+/* 1-D flattened mode (one line per tensor) */
+void launch_dwt1_level(const float* x, int64_t N, const Taps& tp, float* a, float* d, hipStream_t s);
+void launch_idwt1_level(const float* a, int a_thr, const float* d, int64_t N, const Taps& tp, const float* thr,
+                        float* y, int64_t outN, unsigned long long* zc, hipStream_t s);
 void launch_synth(float* out, int64_t n, uint64_t seed, uint32_t tid, int e, hipStream_t s);
 
 }  // namespace wtp

@@ -80,10 +80,10 @@ def percentile_based_thresholding(coeff_arr, percentile=90):
     return out.to(dev)
 
 
-def _run(weights, wavelet, level, percentile, carry_level, verbose):
+def _run(weights, wavelet, level, percentile, carry_level, verbose, flatten=False):
     devs = [w.device for w in weights]
     dev_w = [_cuda(w.detach()) for w in weights]
-    outs, recs = engine.prune(dev_w, wavelet, level, percentile, carry_level=carry_level)
+    outs, recs = engine.prune(dev_w, wavelet, level, percentile, carry_level=carry_level, flatten=flatten)
     outs = [o.to(d) for o, d in zip(outs, devs)]
     if verbose:
         for r in recs:
@@ -91,9 +91,11 @@ def _run(weights, wavelet, level, percentile, carry_level, verbose):
     return outs, recs
 
 
-def _mismatches(weights, recs):
+def _mismatches(weights, recs, flatten=False):
     n = 0
     for w, r in zip(weights, recs):
+        if flatten:  # one line of numel samples: odd lengths are cut back silently
+            continue
         if w.dim() >= 2 and r["eff_level"] > 0:
             h, wd = w.shape[-2], w.shape[-1]
             if h % 2 or wd % 2:
@@ -102,16 +104,20 @@ def _mismatches(weights, recs):
 
 
 def multi_resolution_analysis(weights: List[torch.Tensor], wavelet: str, level: int, percentile: float,
-                              mode: str = "periodization", verbose: bool = True) -> Tuple[List[torch.Tensor], int]:
+                              mode: str = "periodization", verbose: bool = True,
+                              flatten: bool = False) -> Tuple[List[torch.Tensor], int]:
     """Wavelet-domain percentile pruning of each tensor (dwt_pruning.py:35-95).
-    Returns (pruned tensors on their original devices, total count of exact zeros)."""
+    Returns (pruned tensors on their original devices, total count of exact zeros).
+    flatten=True (an extension, not in the reference): the 1-D pywt.wavedec / waverec of every
+    ndim >= 2 tensor's flattened weights instead of the 2-D transform over its last two axes
+    (WTP_FLATTEN, include/wtprune.h)."""
     if mode != "periodization":
         raise NotImplementedError("only mode='periodization' is implemented (the reference's only mode)")
     if len(weights) == 0:
         return [], 0
     with torch.no_grad():
-        outs, recs = _run(list(weights), wavelet, level, percentile, True, verbose)
-    mism = _mismatches(weights, recs)
+        outs, recs = _run(list(weights), wavelet, level, percentile, True, verbose, flatten)
+    mism = _mismatches(weights, recs, flatten)
     if mism > 0:
         print(f"Warning: Shape mismatch occurred in {mism} weights")
     outs = [o.to(dtype=w.dtype).view(w.shape) for o, w in zip(outs, weights)]
@@ -119,12 +125,13 @@ def multi_resolution_analysis(weights: List[torch.Tensor], wavelet: str, level: 
 
 
 def prune_layer_weights(layer: nn.Module, wavelet: str, level: int, percentile: float,
-                        verbose: bool = True) -> Tuple[int, int, int]:
+                        verbose: bool = True, flatten: bool = False) -> Tuple[int, int, int]:
     """Prune layer.weight in place (the bias is untouched); returns (numel, non-zero after,
     zero count) -- dwt_pruning.py:98-127."""
     with torch.no_grad():
         w = layer.weight
-        pruned, zero_count = multi_resolution_analysis([w], wavelet, level, percentile, verbose=verbose)
+        pruned, zero_count = multi_resolution_analysis([w], wavelet, level, percentile, verbose=verbose,
+                                                       flatten=flatten)
         original = w.numel()
         nonzero = int(torch.count_nonzero(pruned[0]).item())
         if verbose:
@@ -134,7 +141,7 @@ def prune_layer_weights(layer: nn.Module, wavelet: str, level: int, percentile: 
 
 
 def wavelet_pruning(model, wavelet: str, level: int, percentile: float, csv_path: str, guid: str,
-                    verbose: bool = True) -> str:
+                    verbose: bool = True, flatten: bool = False) -> str:
     """Prune every Conv2d weight of `model`, log per layer, save the model and append the run
     to the experiment log; returns the per-layer log path (dwt_pruning.py:130-174).
     All layers go through ONE batched device launch sequence (each layer keeps its own
@@ -149,14 +156,14 @@ def wavelet_pruning(model, wavelet: str, level: int, percentile: float, csv_path
     total_nonzero = 0
     with torch.no_grad():
         weights = [m.weight for _, m in convs]
-        outs, recs = _run(weights, wavelet, level, percentile, False, False) if convs else ([], [])
+        outs, recs = _run(weights, wavelet, level, percentile, False, False, flatten) if convs else ([], [])
         for (name, m), out, rec in zip(convs, outs, recs):
             m.weight.data = out.to(dtype=m.weight.dtype).view(m.weight.shape)
             numel, zeros = rec["numel"], rec["zero_count"]
             nonzero = numel - zeros
             if verbose:  # the reference's per-layer output order (:29-30, :91-93, :121-122)
                 _print_threshold_line(percentile, rec)
-                if _mismatches([out], [rec]):
+                if _mismatches([out], [rec], flatten):
                     print("Warning: Shape mismatch occurred in 1 weights")
                 print(f"Original Param Count: {numel}, Non-zero Params: {nonzero}, Total Pruned Count: {zeros}")
             total_pruned += zeros

@@ -89,12 +89,15 @@ def check_tensors(tensors):
             raise TypeError("wavelettransforms_amd: float32 weights only (got %s)" % x.dtype)
 
 
-def launch(tensors, wavelet, level, pct, outs=None, carry_level=True, stream=None):
+WTP_CARRY_LEVEL, WTP_FLATTEN = 1, 2  # include/wtprune.h
+
+
+def launch(tensors, wavelet, level, pct, outs=None, carry_level=True, stream=None, flatten=False):
     """Enqueue the path for `tensors` (CUDA float32) on `stream` (default: current stream).
     Returns (outs, results_dev) without synchronising; results_dev is a uint8 CUDA tensor of
     len(tensors) wtp_result records.  carry_level=True is multi_resolution_analysis over a
     list (the clamped level carries over, dwt_pruning.py:64-65); False is one call per layer
-    (prune_layer_weights / wavelet_pruning)."""
+    (prune_layer_weights / wavelet_pruning).  flatten=True: the 1-D flattened mode (WTP_FLATTEN)."""
     check_tensors(tensors)
     tensors = [x.contiguous() for x in tensors]
     if outs is None:
@@ -106,14 +109,14 @@ def launch(tensors, wavelet, level, pct, outs=None, carry_level=True, stream=Non
     L = N.lib()
     wid = wavelet_id(wavelet)
     desc = _as_desc(tensors, outs)
-    nbytes = L.wtp_workspace_size(desc, n, wid, int(level))
+    flags = (WTP_CARRY_LEVEL if carry_level else 0) | (WTP_FLATTEN if flatten else 0)
+    nbytes = L.wtp_workspace_size_ex(desc, n, wid, int(level), flags)
     ws = workspace(device, nbytes if nbytes else 256)
     res = torch.empty(n * N.RESULT_BYTES, dtype=torch.uint8, device=device)
     if stream is None:
         stream = torch.cuda.current_stream(device)
-    fn = L.wtp_prune_f32 if carry_level else L.wtp_prune_layers_f32
-    rc = fn(desc, n, wid, int(level), float(pct), ws.data_ptr(), ws.numel(), res.data_ptr(),
-            ctypes.c_void_p(stream.cuda_stream))
+    rc = L.wtp_prune_ex_f32(desc, n, wid, int(level), float(pct), flags, ws.data_ptr(), ws.numel(), res.data_ptr(),
+                            ctypes.c_void_p(stream.cuda_stream))
     if rc != N.WTP_OK:
         raise_for(rc, tensors, wavelet)
     return outs, res
@@ -147,9 +150,9 @@ def resident_capacity():
     return int(N.lib().wtp_resident_capacity())
 
 
-def prune(tensors, wavelet, level, pct, outs=None, carry_level=True):
+def prune(tensors, wavelet, level, pct, outs=None, carry_level=True, flatten=False):
     """launch() + wait + decoded per-tensor records (numel, zero_count, nonzero, thr64, ...)."""
-    outs, res = launch(tensors, wavelet, level, pct, outs=outs, carry_level=carry_level)
+    outs, res = launch(tensors, wavelet, level, pct, outs=outs, carry_level=carry_level, flatten=flatten)
     if res is None:
         return outs, []
     return outs, decode(res, len(tensors))
