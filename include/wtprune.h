@@ -142,6 +142,19 @@ size_t wtp_min_prune_workspace_size(const wtp_tensor* tensors, int ntensors, dou
 int wtp_min_prune_f32(const wtp_tensor* tensors, int ntensors, double fraction, void* workspace,
                       size_t workspace_bytes, wtp_result* results_dev, wtp_stream_t stream);
 
+/* random_pruning (ResNet/random_pruning.py:49-56) for a batch of tensors: in tensor t zero
+ * prune_counts[t] (host array; torch.randperm(numel)[:k] slicing: k > numel takes all, k < 0
+ * takes numel + k) distinct flat positions drawn by a keyed pseudo-random permutation of
+ * [0, numel) (csrc/wt_perm.h; seed + tensor index).  torch's Philox stream is not reproduced:
+ * the positions differ from the reference's, the counts follow the same rule.  out may alias
+ * in.  Results: numel and zero_count (zeros of out, NaN counted as non-zero). */
+int wtp_random_prune_f32(const wtp_tensor* tensors, int ntensors, const int64_t* prune_counts, uint64_t seed,
+                         wtp_result* results_dev, wtp_stream_t stream);
+
+/* calculate_sparsity's count (testing_suite/eval_model.py:7-20): *count_dev = #(|x| < thr) over n
+ * device floats (NaN is not counted). */
+int wtp_count_small_f32(const float* x, int64_t n, float thr, unsigned long long* count_dev, wtp_stream_t stream);
+
 /* measurement hook (bench.py): hipEvent_t handles recorded on the call's stream at the stage
  * boundaries of later wtp_prune*_f32 calls on this thread -- [0] start, [1] forward DWT done,
  * [2] k_window, [3] k_collect, [4] k_mask_select, [5] inverse DWT done (first segment group).

@@ -83,6 +83,8 @@ def lib():
         L.or_synth_fill.argtypes = [f32p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32,
                                     ctypes.c_int]
         L.or_min_prune.argtypes = [f32p, f32p, ctypes.c_int64, ctypes.c_double, i64p, f32p]
+        L.or_random_prune.argtypes = [f32p, f32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64,
+                                      ctypes.c_uint32, i64p]
         _lib = L
     return _lib
 
@@ -268,6 +270,18 @@ def min_prune(x, fraction):
         raise RuntimeError("selected index k out of range")
     _check(rc)
     return out, z.value, t.value
+
+
+def random_prune(x, k, seed, tensor_id):
+    """random_pruning's per-layer step (random_pruning.py:53-56) with the keyed permutation of
+    csrc/wt_perm.h in place of torch.randperm; returns (out, zero_count)."""
+    x = np.require(np.asarray(x, np.float32), requirements="C")
+    out = np.empty_like(x)
+    z = ctypes.c_int64()
+    rc = lib().or_random_prune(_f32p(x.reshape(-1)) if x.size else None, _f32p(out.reshape(-1)) if x.size else None,
+                               x.size, int(k), int(seed), int(tensor_id), ctypes.byref(z))
+    _check(rc)
+    return out, z.value
 
 
 def synth(shape, seed, tensor_id, e):

@@ -37,6 +37,7 @@
 
 #include "../wavelettransforms_amd/csrc/wt_filters.inc"
 #include "../wavelettransforms_amd/csrc/wt_synth.h"
+#include "../wavelettransforms_amd/csrc/wt_perm.h"
 
 #define OR_OK 0
 #define OR_EBADWAVELET (-1)  /* pywt.Wavelet(name) -> ValueError                      */
@@ -526,6 +527,23 @@ int or_prune_tensor_flat(const float* in, float* out, int ndim, const int64_t* s
     res->zero_count = z;
     res->nonzero = N - z;
     return res->status = OR_OK;
+}
+
+/* random_pruning (ResNet/random_pruning.py:49-56) restated: torch.randperm(n)[:k] with
+ * Python's slice rule for k, the positions drawn from the keyed permutation of wt_perm.h
+ * (torch's Philox stream is not reproduced), flatten_weights[idx] = 0, count_nonzero. */
+int or_random_prune(const float* in, float* out, int64_t n, int64_t k, uint64_t seed, uint32_t tensor_id,
+                    int64_t* zero_count) {
+    if (n < 0) return OR_EEMPTY;
+    const int64_t keff = k >= 0 ? (k < n ? k : n) : (n + k > 0 ? n + k : 0);
+    if (n > 0 && out != in) memcpy(out, in, sizeof(float) * (size_t)n);
+    const uint64_t key = wt_perm_key(seed, tensor_id);
+    const int h = wt_perm_half_bits((uint64_t)n);
+    for (int64_t j = 0; j < keff; ++j) out[wt_perm((uint64_t)j, (uint64_t)n, h, key)] = 0.0f;
+    int64_t z = 0;
+    for (int64_t i = 0; i < n; ++i) z += out[i] == 0.0f;
+    *zero_count = z;
+    return OR_OK;
 }
 
 /* A batch of independent tensors (one pruning "step" of the CPU baseline), threaded over

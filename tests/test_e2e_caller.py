@@ -1,7 +1,7 @@
 """End-to-end caller run: what main_pruning.py does with this path --
 a Hugging Face ResNet-18 (the reference's model family and layer names, random init: the
 pretrained weights are not available offline) through wavelet_pruning (selective log, saved
-model, experiment log) and then the min-weight baseline -- on the GPU, checked layer by layer
+model, experiment log) and then the random and min-weight baselines -- on the GPU, checked layer by layer
 against the CPU oracle and against the count rules the reference's stored logs follow."""
 import copy
 import csv
@@ -28,8 +28,10 @@ def test_main_pruning_sequence(tmp_path, capsys):
     assert torch.cuda.is_available()
     from wavelettransforms_amd.dwt_pruning import wavelet_pruning
     from wavelettransforms_amd.min_weight_pruning import min_weight_pruning
+    from wavelettransforms_amd.random_pruning import random_pruning
     model = _resnet18()
     min_model = copy.deepcopy(model)
+    rand_model = copy.deepcopy(model)
     convs = [(n, m) for n, m in model.named_modules() if isinstance(m, torch.nn.Conv2d)]
     before = {n: m.weight.detach().cpu().numpy().copy() for n, m in convs}
     work = tmp_path / "a" / "b"  # outputs go to <cwd>/../../WaveletTransforms/ResNet/SavedModels
@@ -39,6 +41,7 @@ def test_main_pruning_sequence(tmp_path, capsys):
     try:
         exp_csv = str(tmp_path / "experiment_log.csv")
         log_path = wavelet_pruning(model, "bior4.4", 5, 0.382 * 100, exp_csv, "e2e0guid")   # main_pruning.py:185
+        random_pruning(rand_model, log_path, "e2e0guid", "bior4.4", 5, 0.382, exp_csv)       # :191-199
         min_weight_pruning(min_model, log_path, "e2e0guid", "bior4.4", 5, 0.382, exp_csv)    # :200-208
     finally:
         os.chdir(cwd)
@@ -69,5 +72,11 @@ def test_main_pruning_sequence(tmp_path, capsys):
     for r, (name, m) in zip(mins, [(n, m) for n, m in min_model.named_modules() if isinstance(m, torch.nn.Conv2d)]):
         n = int(r["Original Parameter Count"])
         assert int(r["Total Pruned Count"]) == int(n * p) == int((m.weight == 0).sum()), name
-    assert exp[2][4] == "min"
+    # the random baseline: pruned == the selective count of each layer (the stored logs' rule)
+    rands = list(csv.DictReader(open(root / "random_pruned" / "log.csv")))
+    for r, s, (name, m) in zip(rands, rows, [(n, m) for n, m in rand_model.named_modules()
+                                              if isinstance(m, torch.nn.Conv2d)]):
+        assert r["Layer Name"] == name
+        assert int(r["Total Pruned Count"]) == int(s["Total Pruned Count"]) == int((m.weight == 0).sum()), name
+    assert [e[4] for e in exp[1:]] == ["selective", "random", "min"]
     assert "Selectively pruned model saved at" in out and "Minimum weight pruning completed." in out

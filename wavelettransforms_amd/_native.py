@@ -77,6 +77,8 @@ def lib():
             "wtp_set_stage_events": ([ctypes.POINTER(ctypes.c_void_p), i32], i32),
             "wtp_min_prune_workspace_size": ([tp, i32, f64], sz),
             "wtp_min_prune_f32": ([tp, i32, f64, vp, sz, vp, vp], i32),
+            "wtp_random_prune_f32": ([tp, i32, ctypes.POINTER(i64), ctypes.c_uint64, vp, vp], i32),
+            "wtp_count_small_f32": ([vp, i64, ctypes.c_float, vp, vp], i32),
             "wtp_set_resident": ([i32], i32),
             "wtp_resident_capacity": ([], i32),
             "wtp_last_error": ([], ctypes.c_char_p),

@@ -15,6 +15,7 @@
 
 #include "wtp_internal.h"
 #include "wt_filters.inc"
+#include "wt_perm.h"
 
 using namespace wtp;
 
@@ -685,6 +686,66 @@ int wtp_min_prune_f32(const wtp_tensor* tensors, int ntensors, double fraction, 
         launch_collect(tab, head, cand, results, s);
         launch_minprune(tab, head, cand, results, thr_t, mp, tiecnt, s);
     }
+    return check_launch();
+}
+
+/* ---------------------------------------------------------- random pruning --- */
+int wtp_random_prune_f32(const wtp_tensor* tensors, int ntensors, const int64_t* prune_counts, uint64_t seed,
+                         wtp_result* results, wtp_stream_t stream) {
+    g_err.clear();
+    g_err_tensor = -1;
+    if (ntensors < 0 || (ntensors > 0 && (!tensors || !results || !prune_counts))) return fail(WTP_EARG, -1, "bad arguments");
+    if (ntensors == 0) return WTP_OK;
+    std::vector<int64_t> numel(ntensors), keff(ntensors);
+    for (int t = 0; t < ntensors; ++t) {
+        const wtp_tensor& x = tensors[t];
+        if (x.ndim < 0 || x.ndim > WTP_MAX_DIMS) return fail(WTP_EARG, t, "tensor %d: ndim %d unsupported", t, x.ndim);
+        int64_t n = 1;
+        for (int d = 0; d < x.ndim; ++d) {
+            if (x.shape[d] < 0) return fail(WTP_EARG, t, "tensor %d: negative dimension", t);
+            n *= x.shape[d];
+        }
+        if (n > 0 && (!x.in || !x.out)) return fail(WTP_EARG, t, "tensor %d: null pointer", t);
+        const int64_t k = prune_counts[t];
+        numel[t] = n;
+        keff[t] = k >= 0 ? std::min(k, n) : std::max<int64_t>(0, n + k); /* randperm(n)[:k], Python slicing */
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(results, 0, sizeof(wtp_result) * (size_t)ntensors, s) != hipSuccess)
+        return fail(WTP_EHIP, -1, "hipMemsetAsync failed");
+    for (int g0 = 0; g0 < ntensors; g0 += SEG_PER_LAUNCH) {
+        RandTable tab;
+        memset(&tab, 0, sizeof tab);
+        int cb = 0, zb = 0;
+        for (int t = g0; t < ntensors && t < g0 + SEG_PER_LAUNCH; ++t) {
+            RandSeg& sg = tab.s[tab.nseg];
+            sg.in = tensors[t].in;
+            sg.out = tensors[t].out;
+            sg.numel = numel[t];
+            sg.k = keff[t];
+            sg.key = wt_perm_key(seed, (uint32_t)t);
+            sg.h = wt_perm_half_bits((uint64_t)numel[t]);
+            sg.res = t;
+            tab.copy_begin[tab.nseg] = cb;
+            tab.zero_begin[tab.nseg] = zb;
+            cb += (int)((numel[t] + CHUNK - 1) / CHUNK);
+            zb += (int)((keff[t] + STREAM_THREADS - 1) / STREAM_THREADS);
+            ++tab.nseg;
+        }
+        tab.copy_begin[tab.nseg] = cb;
+        tab.zero_begin[tab.nseg] = zb;
+        for (int i = tab.nseg + 1; i <= SEG_PER_LAUNCH; ++i) { tab.copy_begin[i] = cb; tab.zero_begin[i] = zb; }
+        launch_random_prune(tab, results, s);
+    }
+    return check_launch();
+}
+
+int wtp_count_small_f32(const float* x, int64_t n, float thr, unsigned long long* count_dev, wtp_stream_t stream) {
+    if (n < 0 || (n > 0 && !x) || !count_dev) return fail(WTP_EARG, -1, "bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(count_dev, 0, sizeof(unsigned long long), s) != hipSuccess)
+        return fail(WTP_EHIP, -1, "hipMemsetAsync failed");
+    if (n > 0) launch_count_small(x, n, thr, count_dev, s);
     return check_launch();
 }
 

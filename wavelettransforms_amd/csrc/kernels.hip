@@ -21,6 +21,7 @@
  */
 #include "wtp_internal.h"
 #include "wt_synth.h"
+#include "wt_perm.h"
 
 #include <atomic>
 #include <cstdlib>
@@ -1717,6 +1718,60 @@ __global__ __launch_bounds__(DWT_THREADS) void k_synth(float* __restrict__ out, 
         out[i] = wt_synth_value(seed, tid, (uint64_t)i, e);
 }
 
+/* ------------------------------------------------------ random pruning --- */
+/* random_pruning (ResNet/random_pruning.py:49-56): out = in with k distinct flat positions
+ * zeroed -- perm(0..k-1) of the keyed permutation in wt_perm.h; zero_count = zeros(in) + the
+ * chosen positions that held a non-zero (count_nonzero counts NaN as non-zero).
+ *   k_rand_copy  out = in (unless in place), zeros(in) per block, the record's numel
+ *   k_rand_zero  one thread per chosen position; block sums of the non-zeros it removed */
+__device__ __forceinline__ int rand_seg(const int32_t* begin, int nseg, int b) {
+    int s = 0;
+    for (int i = 1; i < nseg; ++i) s += b >= begin[i];
+    return s;
+}
+
+__global__ __launch_bounds__(STREAM_THREADS) void k_rand_copy(RandTable t, wtp_result* __restrict__ res) {
+    const int si = rand_seg(t.copy_begin, t.nseg, blockIdx.x);
+    const RandSeg& sg = t.s[si];
+    const int64_t base = (int64_t)(blockIdx.x - t.copy_begin[si]) * CHUNK;
+    const int64_t end = min(sg.numel, base + CHUNK);
+    uint32_t z = 0;
+    for (int64_t i = base + threadIdx.x; i < end; i += STREAM_THREADS) {
+        const float v = sg.in[i];
+        z += v == 0.0f;
+        if (sg.out != sg.in) sg.out[i] = v;
+    }
+    const unsigned long long tot = block_sum_u64<STREAM_THREADS>(z);
+    if (threadIdx.x == 0) {
+        if (tot) atomicAdd((unsigned long long*)&res[sg.res].zero_count, tot);
+        if (base == 0) res[sg.res].numel = sg.numel;
+    }
+}
+
+__global__ __launch_bounds__(STREAM_THREADS) void k_rand_zero(RandTable t, wtp_result* __restrict__ res) {
+    const int si = rand_seg(t.zero_begin, t.nseg, blockIdx.x);
+    const RandSeg& sg = t.s[si];
+    const int64_t j = (int64_t)(blockIdx.x - t.zero_begin[si]) * STREAM_THREADS + threadIdx.x;
+    uint32_t hit = 0;
+    if (j < sg.k) {
+        const int64_t idx = (int64_t)wt_perm((uint64_t)j, (uint64_t)sg.numel, sg.h, sg.key);
+        hit = sg.in[idx] != 0.0f; /* distinct positions: in place, nobody else has written idx */
+        sg.out[idx] = 0.0f;
+    }
+    const unsigned long long tot = block_sum_u64<STREAM_THREADS>(hit);
+    if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long*)&res[sg.res].zero_count, tot);
+}
+
+/* calculate_sparsity (testing_suite/eval_model.py:7-20): #(|x| < thr) of one tensor */
+__global__ __launch_bounds__(STREAM_THREADS) void k_count_small(const float* __restrict__ x, int64_t n, float thr,
+                                                                unsigned long long* __restrict__ count) {
+    uint32_t c = 0;
+    for (int64_t i = (int64_t)blockIdx.x * STREAM_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * STREAM_THREADS)
+        c += fabsf(x[i]) < thr;
+    const unsigned long long tot = block_sum_u64<STREAM_THREADS>(c);
+    if (threadIdx.x == 0 && tot) atomicAdd(count, tot);
+}
+
 /* ---------------------------------------------------------------- launchers --- */
 static inline unsigned grid_for(int64_t total) {
     int64_t g = (total + DWT_THREADS - 1) / DWT_THREADS;
@@ -1804,6 +1859,18 @@ void launch_idwt1_level(const float* a, int a_thr, const float* d, int64_t N, co
 void launch_copy_threshold(const float* P, float* out, int64_t n, const float* thr, unsigned long long* zc,
                            hipStream_t s) {
     hipLaunchKernelGGL(k_copy_threshold, dim3(grid_for(n)), dim3(DWT_THREADS), 0, s, P, out, n, thr, zc);
+}
+void launch_random_prune(const RandTable& t, wtp_result* res, hipStream_t s) {
+    if (t.copy_begin[t.nseg] > 0)
+        hipLaunchKernelGGL(k_rand_copy, dim3(t.copy_begin[t.nseg]), dim3(STREAM_THREADS), 0, s, t, res);
+    if (t.zero_begin[t.nseg] > 0)
+        hipLaunchKernelGGL(k_rand_zero, dim3(t.zero_begin[t.nseg]), dim3(STREAM_THREADS), 0, s, t, res);
+}
+void launch_count_small(const float* x, int64_t n, float thr, unsigned long long* count, hipStream_t s) {
+    int64_t g = (n + STREAM_THREADS * 16 - 1) / (STREAM_THREADS * 16);
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(k_count_small, dim3((unsigned)g), dim3(STREAM_THREADS), 0, s, x, n, thr, count);
 }
 void launch_synth(float* out, int64_t n, uint64_t seed, uint32_t tid, int e, hipStream_t s) {
     hipLaunchKernelGGL(k_synth, dim3(grid_for(n)), dim3(DWT_THREADS), 0, s, out, n, seed, tid, e);

@@ -220,6 +220,25 @@ void launch_inv_level(const float* a_src, int64_t a_bs, int64_t lda, int a_from_
                       hipStream_t s);
 void launch_copy_threshold(const float* P, float* out, int64_t n, const float* thr, unsigned long long* zc,
                            hipStream_t s);
+/* random pruning: one segment per tensor, block ranges per kernel */
+struct RandSeg {
+    const float* in;
+    float* out;
+    int64_t numel;
+    int64_t k;     /* positions to zero (torch.randperm(n)[:prune_count] semantics) */
+    uint64_t key;  /* wt_perm_key(seed, tensor index) */
+    int32_t h;     /* wt_perm_half_bits(numel) */
+    int32_t res;
+};
+struct RandTable {
+    int32_t nseg;
+    int32_t pad;
+    int32_t copy_begin[SEG_PER_LAUNCH + 1]; /* k_rand_copy blocks of CHUNK elements */
+    int32_t zero_begin[SEG_PER_LAUNCH + 1]; /* k_rand_zero blocks of STREAM_THREADS positions */
+    RandSeg s[SEG_PER_LAUNCH];
+};
+void launch_random_prune(const RandTable& t, wtp_result* res, hipStream_t s);
+void launch_count_small(const float* x, int64_t n, float thr, unsigned long long* count, hipStream_t s);
 /* 1-D flattened mode (one line per tensor) */
 void launch_dwt1_level(const float* x, int64_t N, const Taps& tp, float* a, float* d, hipStream_t s);
 void launch_idwt1_level(const float* a, int a_thr, const float* d, int64_t N, const Taps& tp, const float* thr,

@@ -187,6 +187,43 @@ def min_prune(tensors, fraction, outs=None):
     return outs, decode(res, n)
 
 
+def random_prune(tensors, prune_counts, seed, outs=None):
+    """random_pruning's per-layer step (random_pruning.py:53-56) for every tensor (CUDA float32)
+    in one launch sequence: zero randperm(numel)[:k] -- k distinct flat positions of a keyed
+    permutation (csrc/wt_perm.h; tensor index t keys tensor t).  Returns (outs, records)."""
+    check_tensors(tensors)
+    tensors = [x.contiguous() for x in tensors]
+    if outs is None:
+        outs = [torch.empty_like(x) for x in tensors]
+    n = len(tensors)
+    if n == 0:
+        return outs, []
+    if len(prune_counts) != n:
+        raise ValueError("random_prune: %d prune counts for %d tensors" % (len(prune_counts), n))
+    device = tensors[0].device
+    desc = _as_desc(tensors, outs)
+    ks = (ctypes.c_int64 * n)(*[int(k) for k in prune_counts])
+    res = torch.empty(n * N.RESULT_BYTES, dtype=torch.uint8, device=device)
+    rc = N.lib().wtp_random_prune_f32(desc, n, ks, ctypes.c_uint64(int(seed) & (2**64 - 1)), res.data_ptr(),
+                                      ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream))
+    if rc != N.WTP_OK:
+        raise_for(rc, tensors, None)
+    return outs, decode(res, n)
+
+
+def count_small(x, thr):
+    """#(|x| < thr) of a CUDA float32 tensor, thr rounded to float32 as torch's float compare does
+    (calculate_sparsity, testing_suite/eval_model.py:14).  Returns a 0-d int64 CUDA tensor."""
+    check_tensors([x])
+    x = x.contiguous()
+    cnt = torch.empty((), dtype=torch.int64, device=x.device)
+    rc = N.lib().wtp_count_small_f32(x.data_ptr() if x.numel() else None, x.numel(), float(thr), cnt.data_ptr(),
+                                     ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+    if rc != N.WTP_OK:
+        raise RuntimeError(N.last_error())
+    return cnt
+
+
 def threshold(x, pct, out=None):
     """percentile_based_thresholding (dwt_pruning.py:25-32) of a CUDA float32 tensor."""
     check_tensors([x])
