@@ -329,7 +329,8 @@ __device__ __forceinline__ int wave_find_bin(const uint32_t* h, const uint32_t* 
 
 template <int MS>
 __device__ __forceinline__ void window_search_wave(const SegDesc& sd, const uint32_t* h, const uint32_t* hc,
-                                                   uint32_t* kl_out, uint32_t* kh_out, uint32_t* sh_out) {
+                                                   uint32_t* kl_out, uint32_t* kh_out, uint32_t* sh_out,
+                                                   double sig = 6.0, double add = 24.0) {
     const int64_t n = sd.n;
     const bool exact = n <= MS;
     const int m = exact ? (int)n : MS;
@@ -341,7 +342,7 @@ __device__ __forceinline__ void window_search_wave(const SegDesc& sd, const uint
     } else {
         const double p = (double)r0 / (double)(n - 1);
         const double s0 = p * (double)(m - 1), s1 = (double)r1 / (double)(n - 1) * (double)(m - 1);
-        const double d = 6.0 * sqrt((double)m * p * (1.0 - p)) + 24.0;
+        const double d = sig * sqrt((double)m * p * (1.0 - p)) + add;
         sa = (int)floor(s0 - d);
         sb = (int)ceil(s1 + d);
     }
@@ -656,7 +657,8 @@ template <int THREADS, bool COH = false>
 __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st, const uint32_t* __restrict__ cand,
                              wtp_result* __restrict__ res, float* __restrict__ thr_out, uint32_t* stage,
                              int stage_cap, bool publish, uint32_t kl, uint32_t kh, uint32_t sh,
-                             int* path_out = nullptr, uint32_t* hscratch = nullptr, const ResRuns* rr = nullptr) {
+                             int* path_out = nullptr, uint32_t* hscratch = nullptr, const ResRuns* rr = nullptr,
+                             bool prefer_wave = false) {
     __shared__ int sbin[2];
     __shared__ int64_t sbefore[2];
     __shared__ uint32_t lsub[NSUB_MAX];
@@ -796,14 +798,15 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
             const uint64_t lo64 = (uint64_t)kl + 1 + ((uint64_t)blo << sh);
             const uint64_t hi64 = min((uint64_t)kh, (uint64_t)kl + ((uint64_t)(bhi + 1) << sh));
             uint32_t xa = 0, xb = 0;
-            if (in_lds && hscratch && hi64 - lo64 < (uint64_t)(HS_PER * THREADS)) {
+            const bool wave_ok = in_lds && nlo + nhi <= 64 * WSEL_KPL;
+            if (in_lds && hscratch && hi64 - lo64 < (uint64_t)(HS_PER * THREADS) && !(prefer_wave && wave_ok)) {
                 /* one LDS histogram over the bucket's key values: both ranks in one pass */
                 __shared__ uint32_t sx[2], wt[THREADS / 64];
                 block_hist_select<THREADS>(stage, (int)(nlo + nhi), (uint32_t)lo64, (int)(hi64 - lo64 + 1),
                                            (int)(ja - before), (int)(jb - before), hscratch, sx, wt);
                 xa = sx[0];
                 xb = sx[1];
-            } else if (in_lds && nlo + nhi <= 64 * WSEL_KPL) {
+            } else if (wave_ok) {
                 /* a few hundred keys: one wave per rank, a bitwise search in registers */
                 __shared__ uint32_t sx[2];
                 const int wv = threadIdx.x >> 6;
@@ -1158,7 +1161,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     if (wv == 0) {
         uint32_t wkl, wkh, wsh;
         if (WTP_RES_ABL & 1) { wkl = 0x3c000000u; wkh = 0x3c800000u; wsh = 13; }
-        else window_search_wave<M_SAMPLE>(sd, raw, raw + NB, &wkl, &wkh, &wsh);
+        else window_search_wave<M_SAMPLE>(sd, raw, raw + NB, &wkl, &wkh, &wsh, t.pad[1] * 0.01, 8.0);
         if (lane == 0) { s_win[0] = wkl; s_win[1] = wkh; s_win[2] = wsh; }
         WTP_RPROBE(1);
     }
@@ -1276,13 +1279,25 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     __syncthreads();
     WTP_RPROBE(4);
     BarState* bar = bar_region(head, q);
-    if (tid == 0) atomicAdd(&bar->arrive[blockIdx.x & (NSHARD - 1)][0], 1u);
+    const bool selmode = (t.pad[0] & RES_OPT_SELECTOR) != 0;
+    const bool segbar = selmode || (t.pad[0] & RES_OPT_SEGBAR) != 0;
+    const uint32_t nwg_seg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
+    if (tid == 0) {
+        if (segbar) {
+            /* only the segment's workgroups meet; the last arrival of the grid flips the parity
+             * (every workgroup has read it by the time it arrives) */
+            atomicAdd(reinterpret_cast<uint32_t*>(&st->seg_bar[1]), 1u);
+            if (atomicAdd(&bar->arrive[0][0], 1u) == gridDim.x - 1u) stc(&head->parity, q ^ 1u);
+        } else {
+            atomicAdd(&bar->arrive[blockIdx.x & (NSHARD - 1)][0], 1u);
+        }
+    }
     /* ---- speculative store while the other workgroups arrive: unless the window misses, every
      * key < kl is below the threshold and every key > kh above it, so only keys in [kl, kh] are
      * undecided -- write them unpruned now and fix the ones the threshold prunes after the
      * select (in place, the input must stay intact for a possible full-scan select) */
     float* qo = sd.out + base;
-    const bool spec = SPEC && sd.out != sd.data;
+    const bool spec = (SPEC || selmode) && sd.out != sd.data;
     auto store_all = [&](auto&& g) {
         if (FULL) {
             float4* q4 = reinterpret_cast<float4*>(qo);
@@ -1307,21 +1322,49 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     WTP_RPROBE(9);
     /* ---- grid barrier (wait) */
     const int nblk = t.nblk;
-    bool ok = (WTP_RES_ABL & 16) ? true : res_wait(&bar->arrive[0][0], 32,
-                       [&](int s) { return (uint32_t)((nblk - s + NSHARD - 1) / NSHARD); }, NSHARD);
-    WTP_RPROBE(5);
-    if (blockIdx.x == 0 && tid == 0) head->parity = q ^ 1u; /* every workgroup has read it */
-    /* ---- P2 */
     int path = 0;
+    float thr;
+    bool ok;
+    if (selmode) {
+        /* ---- the segment's selector workgroup publishes the threshold (res_selector) */
+        __shared__ uint32_t s_thr[2];
+        if (tid < 64) {
+            const uint64_t t0 = wall_ticks();
+            bool okw = true;
+            while (!__all(ldc<true>(&st->ready) != 0u)) {
+                if (wall_ticks() - t0 > RES_TIMEOUT_TICKS) { okw = false; break; }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (tid == 0) {
+                s_thr[0] = okw ? ldc<true>(&st->thr_bits) : 0u;
+                s_thr[1] = okw ? (uint32_t)ldc<true>(&st->rpath) : (uint32_t)MODE_FAULT;
+            }
+        }
+        __syncthreads();
+        thr = __uint_as_float(s_thr[0]);
+        path = (int)s_thr[1];
+        ok = path != MODE_FAULT;
+        if (!ok) path = MODE_FULL; /* rewrite the whole chunk (the record says MODE_FAULT) */
+        WTP_RPROBE(5);
+        WTP_RPROBE(6);
+    } else {
+    ok = (WTP_RES_ABL & 16) ? true
+            : segbar ? res_wait(reinterpret_cast<const uint32_t*>(&st->seg_bar[1]), 0, [&](int) { return nwg_seg; }, 1)
+                     : res_wait(&bar->arrive[0][0], 32,
+                                [&](int s) { return (uint32_t)((nblk - s + NSHARD - 1) / NSHARD); }, NSHARD);
+    WTP_RPROBE(5);
+    if (!segbar && blockIdx.x == 0 && tid == 0) head->parity = q ^ 1u; /* every workgroup has read it */
+    /* ---- P2 */
     const ResRuns rr{cand, sd.blk_begin, (int)((sd.n + RES_CHUNK - 1) / RES_CHUNK)};
-    const float thr = (WTP_RES_ABL & 8) ? __uint_as_float(kl)
-        : select_body<CT, true>(sd, st, cand, res, thr_out, raw, RES_STAGE, first, kl, kh, sh, &path, wstage, &rr);
+    thr = (WTP_RES_ABL & 8) ? __uint_as_float(kl)
+        : select_body<CT, true>(sd, st, cand, res, thr_out, raw, RES_STAGE, first, kl, kh, sh, &path, wstage, &rr,
+                                (t.pad[0] & RES_OPT_WSEL) != 0);
     WTP_RPROBE(6);
-    if (path == MODE_FULL && !spec) { /* in place: nobody writes before the segment's scans end */
+    }
+    if (!selmode && path == MODE_FULL && !spec) { /* in place: nobody writes before the segment's scans end */
         __syncthreads();
         if (tid == 0) atomicAdd(&st->seg_bar[0], 1ull);
-        const uint32_t nwg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
-        ok = res_wait(reinterpret_cast<const uint32_t*>(&st->seg_bar[0]), 0, [&](int) { return nwg; }, 1) && ok;
+        ok = res_wait(reinterpret_cast<const uint32_t*>(&st->seg_bar[0]), 0, [&](int) { return nwg_seg; }, 1) && ok;
     }
     /* ---- P3: out = where(|x| < thr, 0, x) */
     auto fin = [&](float xv) { return (fabsf(xv) < thr) ? 0.0f : xv; };
@@ -1358,6 +1401,59 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     WTP_RPROBE(7);
 }
 
+/* Selector mode (RES_OPT_SELECTOR): workgroup nblk + s holds no chunk; it derives segment s's
+ * window from the same sample, waits for the segment's data workgroups, resolves the threshold
+ * (select_body over their runs; the full radix select over the input if the window missed),
+ * publishes the record and hands thr / path to the data workgroups through SelState (sc1 stores,
+ * drained, then the `ready` atomic).  Its loads do not queue behind any chunk's stores: the data
+ * workgroups write speculatively meanwhile. */
+__device__ __forceinline__ void res_selector(const SegTable& t, int si, SelHeader* __restrict__ head, uint32_t q,
+                                             uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
+                                             float* __restrict__ thr_out, uint32_t* raw, uint32_t* wstage) {
+    constexpr int CT = RES_THREADS;
+    const SegDesc& sd = t.s[si];
+    SelState* st = sel_region(head, q) + sd.slot;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    BarState* bar = bar_region(head, q);
+    if (tid == 0 && atomicAdd(&bar->arrive[0][0], 1u) == gridDim.x - 1u) stc(&head->parity, q ^ 1u);
+    __shared__ uint32_t s_win[3];
+    {
+        uint32_t ks[M_SAMPLE / CT];
+        sample_keys<CT, M_SAMPLE>(sd, ks);
+        for (int j = tid; j < NB + WCB; j += CT) raw[j] = 0u;
+        const int m = sd.n <= M_SAMPLE ? (int)sd.n : M_SAMPLE;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < M_SAMPLE / CT; ++j)
+            if (j * CT + tid < m) {
+                const int b = key_bin(ks[j]);
+                atomicAdd(&raw[b], 1u);
+                atomicAdd(&raw[NB + (b >> 7)], 1u);
+            }
+        __syncthreads();
+    }
+    if (wv == 0) {
+        uint32_t wkl, wkh, wsh;
+        window_search_wave<M_SAMPLE>(sd, raw, raw + NB, &wkl, &wkh, &wsh, t.pad[1] * 0.01, 8.0);
+        if (lane == 0) { s_win[0] = wkl; s_win[1] = wkh; s_win[2] = wsh; }
+    }
+    __syncthreads();
+    const uint32_t kl = s_win[0], kh = s_win[1], sh = s_win[2];
+    const uint32_t nwg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
+    const bool ok = res_wait(reinterpret_cast<const uint32_t*>(&st->seg_bar[1]), 0, [&](int) { return nwg; }, 1);
+    int path = 0;
+    const ResRuns rr{cand, sd.blk_begin, (int)nwg};
+    const float thr = select_body<CT, true>(sd, st, cand, res, thr_out, raw, RES_STAGE, true, kl, kh, sh, &path,
+                                            wstage, &rr, (t.pad[0] & RES_OPT_WSEL) != 0);
+    if (tid == 0) {
+        stc(&st->thr_bits, __float_as_uint(thr));
+        stc(&st->rpath, ok ? path : (int32_t)MODE_FAULT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        atomicAdd(&st->ready, 1u);
+        if (!ok) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+    }
+}
+
 template <bool SPEC>
 __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader* __restrict__ head,
                                                           uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
@@ -1377,6 +1473,10 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader*
             const int j = (int)blockIdx.x * per + i;
             if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
         }
+    }
+    if ((int)blockIdx.x >= t.nblk) { /* selector mode: one workgroup per segment after the data */
+        res_selector(t, (int)blockIdx.x - t.nblk, head, q, cand, res, thr_out, raw, wstage);
+        return;
     }
     const int si = find_seg(t, blockIdx.x);
     const SegDesc& sd = t.s[si];
@@ -1821,11 +1921,18 @@ int resident_capacity() {
     if (dev < 16) cache[dev].store(cap, std::memory_order_relaxed);
     return cap > 0 ? cap : 0;
 }
-void launch_resident(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
+void launch_resident(const SegTable& t0, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
                      hipStream_t s) {
     static const int spec = [] { const char* e = getenv("WTP_RES_SPEC"); return e ? atoi(e) : 0; }();
-    if (spec) hipLaunchKernelGGL(k_resident<true>, dim3(t.nblk), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
-    else hipLaunchKernelGGL(k_resident<false>, dim3(t.nblk), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
+    static const int opts = [] { const char* e = getenv("WTP_RES_OPTS"); return e ? atoi(e) : RES_OPT_DEFAULT; }();
+    static const int sig = [] { const char* e = getenv("WTP_RES_SIGMA"); return e && atoi(e) > 0 ? atoi(e) : RES_SIGMA_X100; }();
+    SegTable t = t0;
+    t.pad[0] = opts;
+    if ((opts & RES_OPT_SELECTOR) && t.nblk + t.nseg > resident_capacity()) t.pad[0] &= ~RES_OPT_SELECTOR;
+    const int grid = t.nblk + ((t.pad[0] & RES_OPT_SELECTOR) ? t.nseg : 0);
+    t.pad[1] = sig; /* window margin: sig/100 binomial sigma + 8 sample ranks */
+    if (spec) hipLaunchKernelGGL(k_resident<true>, dim3(grid), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
+    else hipLaunchKernelGGL(k_resident<false>, dim3(grid), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
 }
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
                      hipStream_t s) {
