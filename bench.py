@@ -72,14 +72,17 @@ def stage_bytes(stage, n_w, pop, has_dwt):
 
 
 def pmc_traffic(config, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if present."""
-    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % config)
-    try:
-        with open(path) as fh:
-            d = json.load(fh)
-        return d["kernels"][kernel]["hbm_bytes_per_launch"]
-    except Exception:
-        return None
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summaries
+    (profiles/pmc_<config>*.json, FETCH_SIZE x2 + WRITE_SIZE per DESIGN.md), if present."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_%s*.json" % config))):
+        try:
+            with open(path) as fh:
+                d = json.load(fh)
+            return d["kernels"][kernel]["hbm_bytes_per_launch"]
+        except Exception:
+            continue
+    return None
 
 
 def main():

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (binds libamdhip64.so.7 before our library is loaded)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libwtprune.so")
+LIB_PATH = os.environ.get("WTP_LIB_PATH") or os.path.join(HERE, "_lib", "libwtprune.so")  # override: A/B lab builds
 MAX_DIMS = 8
 
 WTP_OK = 0

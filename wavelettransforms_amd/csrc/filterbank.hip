@@ -20,6 +20,7 @@
 #include "wtp_internal.h"
 #include "wt_dwt_core.h"
 
+#include <algorithm>
 #include <cstring>
 
 #pragma clang fp contract(off)
@@ -31,6 +32,14 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 /* timing probes for tools/mb/fblab.hip (empty in the library) */
 #ifndef WTP_FPROBE
 #define WTP_FPROBE(i)
+#endif
+
+/* waves per SIMD the filter-bank kernels are register-budgeted for (db8: 5 needs <= 96 VGPRs) */
+#ifndef WTP_FB_FWD_WPE
+#define WTP_FB_FWD_WPE __attribute__((amdgpu_waves_per_eu(5)))
+#endif
+#ifndef WTP_FB_INV_WPE
+#define WTP_FB_INV_WPE __attribute__((amdgpu_waves_per_eu(5)))
 #endif
 
 constexpr int FB_THREADS = 256;
@@ -264,14 +273,15 @@ struct FwdGroup {
 };
 
 template <int FT>
-__global__ __launch_bounds__(FB_THREADS) void k_fwd_level(FwdGroup g, Taps tp) {
+__global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGroup g, Taps tp) {
     extern __shared__ float lds[];
     const int F = FT ? FT : tp.F;
     const int NR = 2 * FR + F - 2, NC = 2 * FC + F - 2;
     float* T = lds;                /* NR x NC input tile */
-    float2* LH = reinterpret_cast<float2*>(lds + NR * NC); /* FR x NC: (L, H) column-pass outputs,
-                                                              even columns then odd (row-pass reads
-                                                              at stride 2 stay conflict-free) */
+    /* FR x NC: (L, H) column-pass outputs, even columns then odd (row-pass reads at stride 2
+     * stay conflict-free).  Specialised filters hold their column results in registers across
+     * a barrier and write them over the input tile: half the LDS, twice the workgroups per CU */
+    float2* LH = reinterpret_cast<float2*>(FT > 0 ? lds : lds + NR * NC);
     const int HALF = (NC + 1) / 2;
     auto lhi = [&](int o, int cc) { return o * NC + (cc & 1) * HALF + (cc >> 1); };
     const int gt = xcd_tile(blockIdx.x, gridDim.x);
@@ -333,19 +343,32 @@ __global__ __launch_bounds__(FB_THREADS) void k_fwd_level(FwdGroup g, Taps tp) {
         /* one tile column and FR/2 consecutive output rows per item: the column's
          * FR + F - 2 samples are read once into registers and shared by the rows */
         constexpr int RH = FR / 2, NV = 2 * RH + FT - 2, NCc = 2 * FC + FT - 2;
-        for (int it = threadIdx.x; it < 2 * NCc; it += FB_THREADS) {
-            const int h = it >= NCc, cc = it - h * NCc;
-            float v[NV];
+        constexpr int NIT = (2 * NCc + FB_THREADS - 1) / FB_THREADS;
+        f2 res[NIT][RH];
 #pragma unroll
-            for (int k = 0; k < NV; ++k) v[k] = T[(2 * RH * h + k) * NCc + cc];
+        for (int q = 0; q < NIT; ++q) {
+            const int it = threadIdx.x + q * FB_THREADS;
+            if (it < 2 * NCc) {
+                const int h = it >= NCc, cc = it - h * NCc;
+                float v[NV];
 #pragma unroll
-            for (int r = 0; r < RH; ++r) {
-                const int o = RH * h + r;
-                if (o < nrow) {
-                    const int i = FT / 2 + 2 * (o0r + o);
-                    const f2 res = ana2_j<FT>(i, a.R, flo, fhi, [&](int j) { return v[2 * r + FT - 1 - j]; });
-                    LH[lhi(o, cc)] = make_float2(res.x, res.y);
+                for (int k = 0; k < NV; ++k) v[k] = T[(2 * RH * h + k) * NCc + cc];
+#pragma unroll
+                for (int r = 0; r < RH; ++r) {
+                    const int i = FT / 2 + 2 * (o0r + RH * h + r);
+                    res[q][r] = ana2_j<FT>(i, a.R, flo, fhi, [&](int j) { return v[2 * r + FT - 1 - j]; });
                 }
+            }
+        }
+        __syncthreads(); /* every read of T is done: LH overwrites it */
+#pragma unroll
+        for (int q = 0; q < NIT; ++q) {
+            const int it = threadIdx.x + q * FB_THREADS;
+            if (it < 2 * NCc) {
+                const int h = it >= NCc, cc = it - h * NCc;
+#pragma unroll
+                for (int r = 0; r < RH; ++r)
+                    if (RH * h + r < nrow) LH[lhi(RH * h + r, cc)] = make_float2(res[q][r].x, res[q][r].y);
             }
         }
     } else {
@@ -405,7 +428,7 @@ struct InvGroup {
 };
 
 template <int FT>
-__global__ __launch_bounds__(FB_THREADS) void k_inv_level(InvGroup g, Taps tp) {
+__global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGroup g, Taps tp) {
     extern __shared__ float lds[];
     const int F = FT ? FT : tp.F;
     const int H = F / 2;
@@ -421,7 +444,9 @@ __global__ __launch_bounds__(FB_THREADS) void k_inv_level(InvGroup g, Taps tp) {
     const int NRr = r_hi - r_lo + 1, NCc = c_hi - c_lo + 1;
     float2* Aq = reinterpret_cast<float2*>(lds);  /* (cA, cH=da) at each tile position  */
     float2* Dq = Aq + NRr * NCc;                  /* (cV=ad, cD=dd)                     */
-    float2* LoHi = Dq + NRr * NCc;                /* NRr x IC: (lo, hi) row-pass output */
+    /* NRr x IC: (lo, hi) row-pass output; specialised filters keep their rows in registers
+     * across a barrier and write them over Aq/Dq (half the LDS per workgroup) */
+    float2* LoHi = FT > 0 ? Aq : Dq + NRr * NCc;
     const float thr = a.thr ? *a.thr : 0.0f;      /* |c| < 0 never holds: no threshold  */
     auto tl = [&](float c) { return (fabsf(c) < thr) ? 0.0f : c; };
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -476,6 +501,8 @@ __global__ __launch_bounds__(FB_THREADS) void k_inv_level(InvGroup g, Taps tp) {
     const float* rhi = tp.f[3];
     constexpr int HM = FT ? FT / 2 : 1;
     const int m = m0 + lane;
+    constexpr int RRN = (IR / 2 + HM + 2 + 3) / 4; /* rows per wave (NR_MAX / 4) */
+    f2 rowres[FT ? RRN : 1];
     if (lane < IC && m <= ml) {
         const SiteU s = site_u(m, a.C, F);
         auto getA = [&](int rr) {
@@ -495,16 +522,20 @@ __global__ __launch_bounds__(FB_THREADS) void k_inv_level(InvGroup g, Taps tp) {
             auto tl_ = [&](int j) { return tlo[j]; };
             auto th_ = [&](int j) { return thi[j]; };
             const bool inner = __all(!s.special && s.i < a.C);
-            for (int rr = wv; rr < NRr; rr += FB_THREADS / 64) {
-                f2 acc = {0.0f, 0.0f};
-                if (inner) {
-                    acc = syn_pass_inner<FT>(s, F, tl_, getA(rr), acc);
-                    acc = syn_pass_inner<FT>(s, F, th_, getD(rr), acc);
-                } else {
-                    acc = syn_pass_u<FT>(s, a.C, F, tl_, getA(rr), acc);
-                    acc = syn_pass_u<FT>(s, a.C, F, th_, getD(rr), acc);
+#pragma unroll
+            for (int q = 0; q < RRN; ++q) {
+                const int rr = wv + 4 * q;
+                if (rr < NRr) {
+                    f2 acc = {0.0f, 0.0f};
+                    if (inner) {
+                        acc = syn_pass_inner<FT>(s, F, tl_, getA(rr), acc);
+                        acc = syn_pass_inner<FT>(s, F, th_, getD(rr), acc);
+                    } else {
+                        acc = syn_pass_u<FT>(s, a.C, F, tl_, getA(rr), acc);
+                        acc = syn_pass_u<FT>(s, a.C, F, th_, getD(rr), acc);
+                    }
+                    rowres[q] = acc;
                 }
-                LoHi[rr * IC + lane] = make_float2(acc.x, acc.y);
             }
         } else {
             auto tl_ = [&](int j) { return rlo[2 * j + s.par]; };
@@ -517,13 +548,62 @@ __global__ __launch_bounds__(FB_THREADS) void k_inv_level(InvGroup g, Taps tp) {
             }
         }
     }
+    if constexpr (FT > 0) {
+        __syncthreads(); /* every read of Aq/Dq is done: LoHi overwrites them */
+        if (lane < IC && m <= ml) {
+#pragma unroll
+            for (int q = 0; q < RRN; ++q)
+                if (wv + 4 * q < NRr) LoHi[(wv + 4 * q) * IC + lane] = make_float2(rowres[q].x, rowres[q].y);
+        }
+    }
     __syncthreads();
     /* 3. axis -2 synthesis: y = rec_lo over lo, then rec_hi over hi, down each column (the
      *    site of a row is wave-uniform: scalar taps) */
     unsigned long long z = 0;
     if (lane < IC && m <= ml) {
         float* yb = a.y + (int64_t)b * a.outH * a.outW;
-        for (int n = n0 + wv; n <= nl; n += FB_THREADS / 64) {
+        /* specialised filters: each wave owns RB consecutive rows.  Interior blocks run from
+         * registers: outputs k and k + RB/2 share taps (same parity) and sit four sites apart,
+         * so they are computed packed, and each LoHi row is read from LDS once for the block
+         * (H + RB/2 - 1 + E rows instead of H per output) */
+        constexpr int RB = IR / (FB_THREADS / 64);
+        const int nf = FT ? n0 + RB * wv : n0 + wv;
+        const int nend = FT ? min(nf + RB - 1, nl) : nl;
+        const int nstep = FT ? 1 : FB_THREADS / 64;
+        bool fast = false;
+        if constexpr (FT > 0) {
+            constexpr int H = FT / 2, E = (H & 1) ? 0 : 1, NV = H + RB / 2 - 1 + E, RB2 = RB / 2;
+            static_assert(RB % 4 == 0, "packed column blocks pair rows k and k + RB/2, RB/4 sites apart");
+            const SiteU s0 = site_u(nf, a.R, F);
+            const int nlast = nf + RB - 1;
+            fast = nlast <= nl && !s0.special && (E == 0 || nlast < 2 * a.R - 1) &&
+                              s0.i + ((RB - 1 + E) >> 1) < a.R;
+            if (fast) {
+                const int g0 = s0.i - H + 1 - r_lo;
+                float2 r[NV];
+#pragma unroll
+                for (int q = 0; q < NV; ++q) r[q] = LoHi[(g0 + q) * IC + lane];
+#pragma unroll
+                for (int k = 0; k < RB2; ++k) {
+                    const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
+                    f2 acc = {0.0f, 0.0f};
+#pragma unroll
+                    for (int j = 0; j < H; ++j) {
+                        const float t = rlo[2 * j + par];
+                        acc = acc + f2{t, t} * f2{r[base - j].x, r[base - j + RB2 / 2].x};
+                    }
+#pragma unroll
+                    for (int j = 0; j < H; ++j) {
+                        const float t = rhi[2 * j + par];
+                        acc = acc + f2{t, t} * f2{r[base - j].y, r[base - j + RB2 / 2].y};
+                    }
+                    yb[(int64_t)(nf + k) * a.outW + m] = acc.x;
+                    yb[(int64_t)(nf + k + RB2) * a.outW + m] = acc.y;
+                    z += (acc.x == 0.0f) + (acc.y == 0.0f);
+                }
+            }
+        }
+        for (int n = nf; !fast && n <= nend; n += nstep) {
             const SiteU s = site_u(n, a.R, F);
             auto tl_ = [&](int j) { return rlo[2 * j + s.par]; };
             auto th_ = [&](int j) { return rhi[2 * j + s.par]; };
@@ -552,19 +632,24 @@ __global__ __launch_bounds__(FB_THREADS) void k_inv_level(InvGroup g, Taps tp) {
 }
 
 /* ------------------------------------------------------------ launchers --- */
-static size_t fwd_lds(int F) { return sizeof(float) * ((size_t)(2 * FR + F - 2) * (2 * FC + F - 2) + 2 * (size_t)FR * (2 * FC + F - 2)); }
-static size_t inv_lds(int F) {
+/* dynamic LDS per workgroup; `alias`: the specialised kernels write their second-pass input
+ * over their first-pass input (k_fwd_level: LH over T; k_inv_level: LoHi over Aq/Dq) */
+static size_t fwd_lds(int F, bool alias = false) {
+    const size_t t = (size_t)(2 * FR + F - 2) * (2 * FC + F - 2), lh = 2 * (size_t)FR * (2 * FC + F - 2);
+    return sizeof(float) * (alias ? std::max(t, lh) : t + lh);
+}
+static size_t inv_lds(int F, bool alias = false) {
     const size_t nr = IR / 2 + F / 2 + 2, nc = IC / 2 + F / 2 + 2;
-    return sizeof(float) * (4 * nr * nc + 2 * nr * IC);
+    return sizeof(float) * (alias ? std::max(4 * nr * nc, 2 * nr * IC) : 4 * nr * nc + 2 * nr * IC);
 }
 
 template <int FT>
 static void fwd_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
-    hipLaunchKernelGGL(k_fwd_level<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F), s, g, tp);
+    hipLaunchKernelGGL(k_fwd_level<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, FT > 0), s, g, tp);
 }
 template <int FT>
 static void inv_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
-    hipLaunchKernelGGL(k_inv_level<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F), s, g, tp);
+    hipLaunchKernelGGL(k_inv_level<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F, FT > 0), s, g, tp);
 }
 
 /* The tiled path needs an even filter, the LDS budget, and images large enough that a tile
