@@ -353,10 +353,21 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
                 float v[NV];
 #pragma unroll
                 for (int k = 0; k < NV; ++k) v[k] = T[(2 * RH * h + k) * NCc + cc];
+                const int i0 = FT / 2 + 2 * (o0r + RH * h);
+                if (__all(i0 + 2 * (RH - 1) < a.R)) {
+                    /* all RH outputs interior: tap-major, so the RH independent sums interleave */
 #pragma unroll
-                for (int r = 0; r < RH; ++r) {
-                    const int i = FT / 2 + 2 * (o0r + RH * h + r);
-                    res[q][r] = ana2_j<FT>(i, a.R, flo, fhi, [&](int j) { return v[2 * r + FT - 1 - j]; });
+                    for (int r = 0; r < RH; ++r) res[q][r] = f2{0.0f, 0.0f};
+#pragma unroll
+                    for (int j = 0; j < FT; ++j) {
+                        const f2 t = {flo[j], fhi[j]};
+#pragma unroll
+                        for (int r = 0; r < RH; ++r) res[q][r] = res[q][r] + t * v[2 * r + FT - 1 - j];
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < RH; ++r)
+                        res[q][r] = ana2_j<FT>(i0 + 2 * r, a.R, flo, fhi, [&](int j) { return v[2 * r + FT - 1 - j]; });
                 }
             }
         }
@@ -387,20 +398,53 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
     const int oc = o0c + lane;
     if (lane < FC && oc < a.Co) {
         const int i = F / 2 + 2 * oc;
-        for (int o = wv; o < nrow; o += FB_THREADS / 64) {
-            f2 low, high; /* low = (aa, da), high = (ad, dd) */
-            ana2x2<FT>(i, a.C, F, flo, fhi,
-                       [&](int g) {
-                           const float2 v = LH[lhi(o, g - gc0)];
-                           return f2{v.x, v.y};
-                       },
-                       low, high);
+        auto put = [&](int o, f2 low, f2 high) { /* low = (aa, da), high = (ad, dd) */
             const int r = o0r + o;
             if (a.last) Pb[(int64_t)r * a.PC + oc] = low.x;
             else a.anext[((int64_t)b * a.Ro + r) * a.Co + oc] = low.x;
             Pb[(int64_t)r * a.PC + a.offC + oc] = high.x;
             Pb[(int64_t)(a.offR + r) * a.PC + oc] = low.y;
             Pb[(int64_t)(a.offR + r) * a.PC + a.offC + oc] = high.y;
+        };
+        bool done = false;
+        if constexpr (FT > 0) {
+            if (nrow == FR && __all(i < a.C)) {
+                /* full tile, interior columns: two rows at a time, their four sums interleaved */
+                constexpr int NW = FB_THREADS / 64;
+                static_assert(FR % (2 * NW) == 0, "row pairs per wave");
+#pragma unroll
+                for (int pr = 0; pr < FR / (2 * NW); ++pr) {
+                    const int oA = wv + 2 * NW * pr, oB = oA + NW;
+                    f2 vA[FT], vB[FT];
+#pragma unroll
+                    for (int j = 0; j < FT; ++j) {
+                        const float2 xa = LH[lhi(oA, i - j - gc0)], xb = LH[lhi(oB, i - j - gc0)];
+                        vA[j] = f2{xa.x, xa.y};
+                        vB[j] = f2{xb.x, xb.y};
+                    }
+                    f2 aA = {0.0f, 0.0f}, dA = {0.0f, 0.0f}, aB = {0.0f, 0.0f}, dB = {0.0f, 0.0f};
+#pragma unroll
+                    for (int j = 0; j < FT; ++j) {
+                        aA = aA + flo[j] * vA[j];
+                        dA = dA + fhi[j] * vA[j];
+                        aB = aB + flo[j] * vB[j];
+                        dB = dB + fhi[j] * vB[j];
+                    }
+                    put(oA, aA, dA);
+                    put(oB, aB, dB);
+                }
+                done = true;
+            }
+        }
+        for (int o = wv; !done && o < nrow; o += FB_THREADS / 64) {
+            f2 low, high;
+            ana2x2<FT>(i, a.C, F, flo, fhi,
+                       [&](int g) {
+                           const float2 v = LH[lhi(o, g - gc0)];
+                           return f2{v.x, v.y};
+                       },
+                       low, high);
+            put(o, low, high);
         }
     }
     WTP_FPROBE(3);
@@ -430,9 +474,9 @@ struct InvGroup {
 template <int FT>
 __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGroup g, Taps tp) {
     extern __shared__ float lds[];
+    const int gt = xcd_tile(blockIdx.x, gridDim.x);
     const int F = FT ? FT : tp.F;
     const int H = F / 2;
-    const int gt = xcd_tile(blockIdx.x, gridDim.x);
     const int item = find_item(g.blk_begin, gt);
     const auto& a = g.it[item];
     const int tile = gt - g.blk_begin[item];
@@ -452,6 +496,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const float* Pb = a.P + (int64_t)b * a.P_bs;
     const float* ab = a.a + (int64_t)b * a.a_bs;
+    WTP_FPROBE(0);
     /* 1. the four coefficient tiles (periodic wrap, thresholded on load); all loads of a
      *    thread issued before the LDS writes (compile-time trip count) */
     {
@@ -629,6 +674,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
         __syncthreads();
         if (threadIdx.x == 0 && zs) atomicAdd(a.zc, zs);
     }
+    WTP_FPROBE(3);
 }
 
 /* ------------------------------------------------------------ launchers --- */

@@ -383,11 +383,11 @@ __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __rest
     float4 v[IT];
     if constexpr (WIN) {
         /* sample loads first, then the stream loads: the window is built while the chunk arrives */
-        uint32_t ks[M_SAMPLE / CT];
-        sample_keys<CT, M_SAMPLE>(sd, ks);
+        uint32_t ks[M_SAMPLE_WIN / CT];
+        sample_keys<CT, M_SAMPLE_WIN>(sd, ks);
         if (FULL) load_chunk<IT, CT>(p, v);
         else load_chunk_ragged<IT, CT>(p, len, v);
-        window_from_keys<CT, M_SAMPLE>(sd, ks, *wl, &kl, &kh, &sh);
+        window_from_keys<CT, M_SAMPLE_WIN>(sd, ks, *wl, &kl, &kh, &sh);
         if (first && threadIdx.x == 0) { st->kl = kl; st->kh = kh; st->shift = sh; } /* for the select */
     } else {
         /* the window came from k_window; the stream loads go out first (the window words are
@@ -904,10 +904,10 @@ constexpr int WIN_THREADS = 1024;
 __global__ __launch_bounds__(WIN_THREADS) void k_window(SegTable t, SelHeader* __restrict__ head) {
     __shared__ WindowLds<WIN_THREADS> wl;
     const SegDesc& sd = t.s[blockIdx.x];
-    uint32_t ks[M_SAMPLE / WIN_THREADS];
-    sample_keys<WIN_THREADS, M_SAMPLE>(sd, ks);
+    uint32_t ks[M_SAMPLE_WIN / WIN_THREADS];
+    sample_keys<WIN_THREADS, M_SAMPLE_WIN>(sd, ks);
     uint32_t kl, kh, sh;
-    window_from_keys<WIN_THREADS, M_SAMPLE>(sd, ks, wl, &kl, &kh, &sh);
+    window_from_keys<WIN_THREADS, M_SAMPLE_WIN>(sd, ks, wl, &kl, &kh, &sh);
     if (threadIdx.x == 0) {
         SelState* st = sel_region(head, head->parity) + sd.slot;
         st->kl = kl;

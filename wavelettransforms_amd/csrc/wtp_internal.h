@@ -21,7 +21,9 @@ namespace wtp {
  * key-range buckets; k_select reads only the bucket(s) holding the two
  * ranks and resolves them exactly, or by a full radix select over the segment if the window
  * missed. */
-constexpr int M_SAMPLE = 4096;
+constexpr int M_SAMPLE = 4096;      /* k_resident: every workgroup draws it before its chunk    */
+constexpr int M_SAMPLE_WIN = 16384; /* k_window (three-launch form): one block per segment; the
+                                       narrower window halves k_collect's candidate traffic */
 constexpr int SAMPLE_GROUP = 16;   /* contiguous keys per sample group */
 constexpr int NSUB_MAX = 1024;     /* buckets over (kl, kh]: 64..1024 per segment (SegDesc) */
 constexpr int BUCKET_MAX = 8192;   /* keys per bucket (two buckets are staged in LDS)       */
