@@ -6,12 +6,13 @@
 __device__ unsigned long long* g_occ;
 #define WTP_FPROBE(i)                                                                              \
     do {                                                                                           \
-        if (threadIdx.x == 0 && (i == 0 || i == 3)) {                                              \
+        if (threadIdx.x == 0) {                                                                    \
             unsigned hw, xcc;                                                                      \
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));                      \
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));                    \
-            g_occ[3 * gt + (i == 0 ? 0 : 1)] = wall_clock64();                             \
-            if (i == 0) g_occ[3 * gt + 2] = ((unsigned long long)(xcc & 15) << 32) | hw;   \
+            const int slot_ = i == 0 ? 0 : (i == 3 ? 1 : 2 + i);                                   \
+            g_occ[5 * gt + slot_] = wall_clock64();                                                \
+            if (i == 0) g_occ[5 * gt + 2] = ((unsigned long long)(xcc & 15) << 32) | hw;           \
         }                                                                                          \
     } while (0)
 #include "../../wavelettransforms_amd/csrc/filterbank.hip"
@@ -26,9 +27,11 @@ using namespace wtp;
 static void report(const char* name, const unsigned long long* h, int nwg) {
     std::map<unsigned long long, std::vector<std::pair<unsigned long long, int>>> ev; /* cu -> (t, +1/-1) */
     unsigned long long t0 = ~0ull, t1 = 0;
-    std::vector<double> life;
+    std::vector<double> life, p1, p2;
     for (int b = 0; b < nwg; ++b) {
-        const unsigned long long s = h[3 * b], e = h[3 * b + 1], id = h[3 * b + 2];
+        const unsigned long long s = h[5 * b], e = h[5 * b + 1], id = h[5 * b + 2];
+        p1.push_back((h[5 * b + 3] - s) / 100.0);
+        p2.push_back((h[5 * b + 4] - s) / 100.0);
         const unsigned hw = (unsigned)id;
         const unsigned long long cu = ((id >> 32) << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15);
         ev[cu].push_back({s, +1});
@@ -38,6 +41,8 @@ static void report(const char* name, const unsigned long long* h, int nwg) {
         life.push_back((e - s) / 100.0);
     }
     std::sort(life.begin(), life.end());
+    std::sort(p1.begin(), p1.end());
+    std::sort(p2.begin(), p2.end());
     int mx = 0;
     double area = 0;
     for (auto& kv : ev) {
@@ -50,6 +55,7 @@ static void report(const char* name, const unsigned long long* h, int nwg) {
     printf("%-28s WGs %6d CUs %3zu span %8.2f us  life p10/50/90 %6.2f %6.2f %6.2f us  WGs per CU mean %.2f max %d\n",
            name, nwg, ev.size(), (t1 - t0) / 100.0, life[life.size() / 10], life[life.size() / 2], life[9 * life.size() / 10],
            area / ((t1 - t0) * (double)ev.size()), mx);
+    printf("%-28s median probe 1 at %.2f us, probe 2 at %.2f us (from the tile's start)\n", "", p1[p1.size() / 2], p2[p2.size() / 2]);
 }
 
 int main(int argc, char** argv) {
@@ -69,13 +75,13 @@ int main(int argc, char** argv) {
     CK(hipMemset(x, 0, n * 4)); CK(hipMemset(P, 0, (size_t)B * g.PR * g.PC * 4));
     float thr = 0.001f, *dthr; CK(hipMalloc(&dthr, 4)); CK(hipMemcpy(dthr, &thr, 4, hipMemcpyHostToDevice));
     const int MAXWG = 1 << 16;
-    unsigned long long* occ; CK(hipMalloc(&occ, (size_t)3 * MAXWG * 8));
+    unsigned long long* occ; CK(hipMalloc(&occ, (size_t)5 * MAXWG * 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_occ), &occ, sizeof(occ)));
-    std::vector<unsigned long long> h(3 * MAXWG);
+    std::vector<unsigned long long> h(5 * MAXWG);
     auto run = [&](const char* name, auto fn, int nwg) {
         for (int i = 0; i < 3; ++i) fn();
         CK(hipDeviceSynchronize());
-        CK(hipMemcpy(h.data(), occ, (size_t)3 * nwg * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h.data(), occ, (size_t)5 * nwg * 8, hipMemcpyDeviceToHost));
         report(name, h.data(), nwg);
     };
     for (int k = 1; k <= 2; ++k) {

@@ -539,6 +539,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
         }
     }
     __syncthreads();
+    WTP_FPROBE(1);
     /* 2. axis -1 synthesis of every tile row: lo = rec(cA, cV), hi = rec(cH, cD), carried
      *    packed as (lo, hi): rec_lo over (cA, cH), then rec_hi over (cV, cD).  Each lane's
      *    taps (its output parity) are resolved into registers once. */
@@ -566,20 +567,27 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
             }
             auto tl_ = [&](int j) { return tlo[j]; };
             auto th_ = [&](int j) { return thi[j]; };
-            const bool inner = __all(!s.special && s.i < a.C);
+            if (__all(!s.special && s.i < a.C)) {
+                /* interior columns: no branch between the rows (rows past NRr are clamped, computed
+                 * and dropped at the write), so their independent sums interleave */
 #pragma unroll
-            for (int q = 0; q < RRN; ++q) {
-                const int rr = wv + 4 * q;
-                if (rr < NRr) {
+                for (int q = 0; q < RRN; ++q) {
+                    const int rr = min(wv + 4 * q, NRr - 1);
                     f2 acc = {0.0f, 0.0f};
-                    if (inner) {
-                        acc = syn_pass_inner<FT>(s, F, tl_, getA(rr), acc);
-                        acc = syn_pass_inner<FT>(s, F, th_, getD(rr), acc);
-                    } else {
+                    acc = syn_pass_inner<FT>(s, F, tl_, getA(rr), acc);
+                    acc = syn_pass_inner<FT>(s, F, th_, getD(rr), acc);
+                    rowres[q] = acc;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < RRN; ++q) {
+                    const int rr = wv + 4 * q;
+                    if (rr < NRr) {
+                        f2 acc = {0.0f, 0.0f};
                         acc = syn_pass_u<FT>(s, a.C, F, tl_, getA(rr), acc);
                         acc = syn_pass_u<FT>(s, a.C, F, th_, getD(rr), acc);
+                        rowres[q] = acc;
                     }
-                    rowres[q] = acc;
                 }
             }
         } else {
@@ -602,6 +610,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
         }
     }
     __syncthreads();
+    WTP_FPROBE(2);
     /* 3. axis -2 synthesis: y = rec_lo over lo, then rec_hi over hi, down each column (the
      *    site of a row is wave-uniform: scalar taps) */
     unsigned long long z = 0;
