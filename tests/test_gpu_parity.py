@@ -118,7 +118,11 @@ MIXED_SHAPES = [(64, 64), (3, 2, 40, 70), (1, 1, 97, 130), (2, 1, 33, 33), (2, 2
                 (64, 32), (300, 300)]
 
 
-@pytest.mark.parametrize("wavelet", ["haar", "db8", "bior3.3", "coif2", "rbio2.2"])
+# every specialised filter length of the tiled filter bank (F = 2, 4, 6, 8, 10, 12, 16, 18, with
+# H = F/2 odd and even: the packed synthesis-column blocks pair rows by the parity of H), the
+# generic tiled kernels (db7: F = 14, coif4: F = 24) and the per-point kernels (dmey: F = 62)
+@pytest.mark.parametrize("wavelet", ["haar", "db2", "rbio2.2", "bior3.3", "db5", "coif2", "db8", "db9", "db7",
+                                     "coif4", "dmey"])
 def test_grouped_levels_mixed_batch(eng, wavelet):
     """One call over 15 tensors of mixed sizes, batch dims and clamped levels: the same level of
     every tensor runs as one grouped filter-bank launch (more than FB_GROUP images, so the group
