@@ -96,24 +96,28 @@ constexpr size_t PERSIST_BYTES = ((sizeof(SelHeader) + 2 * SEL_REGION) + 255) / 
 bool pct_ok(double pct) { return pct >= 0.0 && pct <= 100.0; }
 
 /* candidate buckets of the three-launch form: ~1000 keys of 5% of the population per bucket
- * (64..1024 buckets; the window holds ~11%, so ~2000) -- long runs per block keep k_collect's
- * scatter in whole lines -- with capacity for 4x that (an overflowing bucket sends the select
- * to its exact full-scan path).  The resident form always uses NSUB_MAX buckets: its runs are
- * per workgroup, and narrow buckets let one LDS histogram finish the select. */
-void bucket_plan(int64_t n, int* nsub_log2, int* bucket_cap) {
+ * (64..1024 buckets; the window holds ~5-6%) with capacity for 4x that (an overflowing bucket
+ * sends the select to its exact full-scan path).  A DWT segment's select runs once (its first
+ * k_mask_select block), so its buckets hold ~2000 keys -- still one LDS stage for the select
+ * (MS_STAGE), twice as long runs per k_collect block (its ~900 inside keys are ~1 key per bucket
+ * at 1024 buckets: partial-line stores, 4x the candidate bytes).  64 buckets cut those stores to
+ * 1.2x but the select then radix-selects ~28K keys from L2 (+55 us per launch on cfg5, more
+ * than k_collect saved).  The resident form always uses NSUB_MAX buckets: its runs are per
+ * workgroup, and narrow buckets let one LDS histogram finish the select. */
+void bucket_plan(int64_t n, int* nsub_log2, int* bucket_cap, bool dwt) {
     const double expect = 0.05 * (double)n;
     int lg = 6;
-    while (lg < 10 && (double)(1 << lg) * 1024.0 < expect) ++lg;
+    while (lg < 10 && (double)(1 << lg) * (dwt ? 2048.0 : 1024.0) < expect) ++lg;
     int64_t bc = (int64_t)(4.0 * expect / (double)(1 << lg)) + 1;
     if (bc < 256) bc = 256;
-    if (bc > BUCKET_MAX) bc = BUCKET_MAX;
+    if (bc > (dwt ? BUCKET_MAX_DWT : BUCKET_MAX)) bc = dwt ? BUCKET_MAX_DWT : BUCKET_MAX;
     *nsub_log2 = lg;
     *bucket_cap = (int)bc;
 }
 
-int64_t cap_for(int64_t n) {
+int64_t cap_for(int64_t n, bool dwt) {
     int lg, bc;
-    bucket_plan(n, &lg, &bc);
+    bucket_plan(n, &lg, &bc, dwt);
     return (int64_t)bc << lg;
 }
 
@@ -190,7 +194,7 @@ int plan_tensors(const wtp_tensor* ts, int n, int wid, int level, double pct, bo
         }
         /* selection counts are kept in 32 bits on the device (8 GiB of float32 per tensor) */
         if (p.pop > (int64_t)INT32_MAX) return fail(WTP_EARG, t, "tensor %d: more than 2^31-1 coefficients", t);
-        p.cap = cap_for(p.pop);
+        p.cap = cap_for(p.pop, p.dwt);
     }
     return WTP_OK;
 }
@@ -516,7 +520,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             if ((a % 16) == 0 && (o % 16) == 0) sd.flags |= SEG_ALIGNED;
             sd.cand_off = (int64_t)p.cand_off;
             sd.cap = p.cap;
-            bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap);
+            bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap, p.dwt);
             if (resident) sd.nsub_log2 = 10; /* NSUB_MAX */
             blk += (int)((p.pop + chunk - 1) / chunk);
         }
@@ -611,7 +615,7 @@ static int plan_min(const wtp_tensor* ts, int n, double fraction, bool check_ptr
             return fail(WTP_EARG, t, "selected index k out of range");
         m.k[t] = (int64_t)kd; /* C cast truncates toward zero, like int() */
         p.pop = p.numel;
-        p.cap = p.numel ? cap_for(p.pop) : 0;
+        p.cap = p.numel ? cap_for(p.pop, false) : 0;
         m.nblk += (int)((p.pop + CHUNK - 1) / CHUNK);
     }
     m.lay = make_layout(m.ps);
@@ -677,7 +681,7 @@ int wtp_min_prune_f32(const wtp_tensor* tensors, int ntensors, double fraction, 
             if ((a % 16) == 0 && (o % 16) == 0) sd.flags |= SEG_ALIGNED;
             sd.cand_off = (int64_t)p.cand_off;
             sd.cap = p.cap;
-            bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap);
+            bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap, false);
             blk += (int)((p.pop + CHUNK - 1) / CHUNK);
         }
         tab.nblk = blk;

@@ -27,6 +27,7 @@ constexpr int M_SAMPLE_WIN = 16384; /* k_window (three-launch form): one block p
 constexpr int SAMPLE_GROUP = 16;   /* contiguous keys per sample group */
 constexpr int NSUB_MAX = 1024;     /* buckets over (kl, kh]: 64..1024 per segment (SegDesc) */
 constexpr int BUCKET_MAX = 8192;   /* keys per bucket (two buckets are staged in LDS)       */
+constexpr int BUCKET_MAX_DWT = 1 << 16; /* DWT segments: 64 wide buckets, one select per segment */
 constexpr int WIN_EXP = 32;
 constexpr int MANT_BITS = 7;
 constexpr uint32_t WIN_E0 = 101;   /* bin window = [2^-26, 2^6) */
