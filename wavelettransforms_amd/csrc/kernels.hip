@@ -1279,8 +1279,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     __syncthreads();
     WTP_RPROBE(4);
     BarState* bar = bar_region(head, q);
-    const bool selmode = (t.pad[0] & RES_OPT_SELECTOR) != 0;
-    const bool segbar = selmode || (t.pad[0] & RES_OPT_SEGBAR) != 0;
+    const bool segbar = (t.pad[0] & RES_OPT_SEGBAR) != 0;
     const uint32_t nwg_seg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
     if (tid == 0) {
         if (segbar) {
@@ -1297,7 +1296,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
      * undecided -- write them unpruned now and fix the ones the threshold prunes after the
      * select (in place, the input must stay intact for a possible full-scan select) */
     float* qo = sd.out + base;
-    const bool spec = (SPEC || selmode) && sd.out != sd.data;
+    const bool spec = SPEC && sd.out != sd.data;
     auto store_all = [&](auto&& g) {
         if (FULL) {
             float4* q4 = reinterpret_cast<float4*>(qo);
@@ -1322,46 +1321,20 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     WTP_RPROBE(9);
     /* ---- grid barrier (wait) */
     const int nblk = t.nblk;
-    int path = 0;
-    float thr;
-    bool ok;
-    if (selmode) {
-        /* ---- the segment's selector workgroup publishes the threshold (res_selector) */
-        __shared__ uint32_t s_thr[2];
-        if (tid < 64) {
-            const uint64_t t0 = wall_ticks();
-            bool okw = true;
-            while (!__all(ldc<true>(&st->ready) != 0u)) {
-                if (wall_ticks() - t0 > RES_TIMEOUT_TICKS) { okw = false; break; }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            if (tid == 0) {
-                s_thr[0] = okw ? ldc<true>(&st->thr_bits) : 0u;
-                s_thr[1] = okw ? (uint32_t)ldc<true>(&st->rpath) : (uint32_t)MODE_FAULT;
-            }
-        }
-        __syncthreads();
-        thr = __uint_as_float(s_thr[0]);
-        path = (int)s_thr[1];
-        ok = path != MODE_FAULT;
-        if (!ok) path = MODE_FULL; /* rewrite the whole chunk (the record says MODE_FAULT) */
-        WTP_RPROBE(5);
-        WTP_RPROBE(6);
-    } else {
-    ok = (WTP_RES_ABL & 16) ? true
+    bool ok = (WTP_RES_ABL & 16) ? true
             : segbar ? res_wait(reinterpret_cast<const uint32_t*>(&st->seg_bar[1]), 0, [&](int) { return nwg_seg; }, 1)
                      : res_wait(&bar->arrive[0][0], 32,
                                 [&](int s) { return (uint32_t)((nblk - s + NSHARD - 1) / NSHARD); }, NSHARD);
     WTP_RPROBE(5);
     if (!segbar && blockIdx.x == 0 && tid == 0) head->parity = q ^ 1u; /* every workgroup has read it */
     /* ---- P2 */
+    int path = 0;
     const ResRuns rr{cand, sd.blk_begin, (int)((sd.n + RES_CHUNK - 1) / RES_CHUNK)};
-    thr = (WTP_RES_ABL & 8) ? __uint_as_float(kl)
+    const float thr = (WTP_RES_ABL & 8) ? __uint_as_float(kl)
         : select_body<CT, true>(sd, st, cand, res, thr_out, raw, RES_STAGE, first, kl, kh, sh, &path, wstage, &rr,
                                 (t.pad[0] & RES_OPT_WSEL) != 0);
     WTP_RPROBE(6);
-    }
-    if (!selmode && path == MODE_FULL && !spec) { /* in place: nobody writes before the segment's scans end */
+    if (path == MODE_FULL && !spec) { /* in place: nobody writes before the segment's scans end */
         __syncthreads();
         if (tid == 0) atomicAdd(&st->seg_bar[0], 1ull);
         ok = res_wait(reinterpret_cast<const uint32_t*>(&st->seg_bar[0]), 0, [&](int) { return nwg_seg; }, 1) && ok;
@@ -1401,59 +1374,6 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     WTP_RPROBE(7);
 }
 
-/* Selector mode (RES_OPT_SELECTOR): workgroup nblk + s holds no chunk; it derives segment s's
- * window from the same sample, waits for the segment's data workgroups, resolves the threshold
- * (select_body over their runs; the full radix select over the input if the window missed),
- * publishes the record and hands thr / path to the data workgroups through SelState (sc1 stores,
- * drained, then the `ready` atomic).  Its loads do not queue behind any chunk's stores: the data
- * workgroups write speculatively meanwhile. */
-__device__ __forceinline__ void res_selector(const SegTable& t, int si, SelHeader* __restrict__ head, uint32_t q,
-                                             uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
-                                             float* __restrict__ thr_out, uint32_t* raw, uint32_t* wstage) {
-    constexpr int CT = RES_THREADS;
-    const SegDesc& sd = t.s[si];
-    SelState* st = sel_region(head, q) + sd.slot;
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    BarState* bar = bar_region(head, q);
-    if (tid == 0 && atomicAdd(&bar->arrive[0][0], 1u) == gridDim.x - 1u) stc(&head->parity, q ^ 1u);
-    __shared__ uint32_t s_win[3];
-    {
-        uint32_t ks[M_SAMPLE / CT];
-        sample_keys<CT, M_SAMPLE>(sd, ks);
-        for (int j = tid; j < NB + WCB; j += CT) raw[j] = 0u;
-        const int m = sd.n <= M_SAMPLE ? (int)sd.n : M_SAMPLE;
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < M_SAMPLE / CT; ++j)
-            if (j * CT + tid < m) {
-                const int b = key_bin(ks[j]);
-                atomicAdd(&raw[b], 1u);
-                atomicAdd(&raw[NB + (b >> 7)], 1u);
-            }
-        __syncthreads();
-    }
-    if (wv == 0) {
-        uint32_t wkl, wkh, wsh;
-        window_search_wave<M_SAMPLE>(sd, raw, raw + NB, &wkl, &wkh, &wsh, t.pad[1] * 0.01, 8.0);
-        if (lane == 0) { s_win[0] = wkl; s_win[1] = wkh; s_win[2] = wsh; }
-    }
-    __syncthreads();
-    const uint32_t kl = s_win[0], kh = s_win[1], sh = s_win[2];
-    const uint32_t nwg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
-    const bool ok = res_wait(reinterpret_cast<const uint32_t*>(&st->seg_bar[1]), 0, [&](int) { return nwg; }, 1);
-    int path = 0;
-    const ResRuns rr{cand, sd.blk_begin, (int)nwg};
-    const float thr = select_body<CT, true>(sd, st, cand, res, thr_out, raw, RES_STAGE, true, kl, kh, sh, &path,
-                                            wstage, &rr, (t.pad[0] & RES_OPT_WSEL) != 0);
-    if (tid == 0) {
-        stc(&st->thr_bits, __float_as_uint(thr));
-        stc(&st->rpath, ok ? path : (int32_t)MODE_FAULT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        atomicAdd(&st->ready, 1u);
-        if (!ok) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
-    }
-}
-
 template <bool SPEC>
 __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader* __restrict__ head,
                                                           uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
@@ -1473,10 +1393,6 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader*
             const int j = (int)blockIdx.x * per + i;
             if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
         }
-    }
-    if ((int)blockIdx.x >= t.nblk) { /* selector mode: one workgroup per segment after the data */
-        res_selector(t, (int)blockIdx.x - t.nblk, head, q, cand, res, thr_out, raw, wstage);
-        return;
     }
     const int si = find_seg(t, blockIdx.x);
     const SegDesc& sd = t.s[si];
@@ -1928,8 +1844,7 @@ void launch_resident(const SegTable& t0, SelHeader* head, uint32_t* cand, wtp_re
     static const int sig = [] { const char* e = getenv("WTP_RES_SIGMA"); return e && atoi(e) > 0 ? atoi(e) : RES_SIGMA_X100; }();
     SegTable t = t0;
     t.pad[0] = opts;
-    if ((opts & RES_OPT_SELECTOR) && t.nblk + t.nseg > resident_capacity()) t.pad[0] &= ~RES_OPT_SELECTOR;
-    const int grid = t.nblk + ((t.pad[0] & RES_OPT_SELECTOR) ? t.nseg : 0);
+    const int grid = t.nblk;
     t.pad[1] = sig; /* window margin: sig/100 binomial sigma + 8 sample ranks */
     if (spec) hipLaunchKernelGGL(k_resident<true>, dim3(grid), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
     else hipLaunchKernelGGL(k_resident<false>, dim3(grid), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);

@@ -115,10 +115,7 @@ struct alignas(128) SelState {
     int32_t mode;                     /* MODE_* chosen by the select (diagnostics)           */
     float thr32;                      /* the float32 threshold the compare uses              */
     uint32_t key_a, key_b;            /* resolved order statistics                           */
-    uint32_t ready;                   /* k_resident selector mode: threshold published (atomic)  */
-    uint32_t thr_bits;                /* ... its float32 bits (sc1 store before `ready`)          */
-    int32_t rpath;                    /* ... and the select's path                                */
-    uint32_t pad1[22];
+    uint32_t pad1[25];
     uint32_t sub[NSUB_MAX];           /* keys per bucket (returning atomicAdd, k_collect)    */
 };
 static_assert(sizeof(SelState) % 128 == 0 && sizeof(SelState) == 4608, "SelState layout");
@@ -170,8 +167,6 @@ constexpr int RES_IT = 24;                          /* float4 per thread held in
 constexpr int RES_CHUNK = RES_THREADS * RES_IT * 4; /* 49152 elements per workgroup   */
 constexpr int RES_OPT_SEGBAR = 1;                   /* segment-wide barriers instead of the grid barrier */
 constexpr int RES_OPT_WSEL = 2;                     /* one wave per rank for <= 1024 staged keys */
-constexpr int RES_OPT_SELECTOR = 4;                 /* one extra workgroup per segment selects; the data
-                                                       workgroups store speculatively meanwhile */
 constexpr int RES_OPT_DEFAULT = RES_OPT_SEGBAR;
 /* k_resident's window margin in binomial sigmas x 100 (+ 8 sample ranks): a miss costs a full
  * scan of the segment, 4 sigma makes that ~1e-4 per segment; the three-launch form keeps 6 + 24 */
