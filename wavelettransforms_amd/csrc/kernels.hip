@@ -383,11 +383,11 @@ __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __rest
     float4 v[IT];
     if constexpr (WIN) {
         /* sample loads first, then the stream loads: the window is built while the chunk arrives */
-        uint32_t ks[M_SAMPLE_WIN / CT];
-        sample_keys<CT, M_SAMPLE_WIN>(sd, ks);
+        uint32_t ks[M_SAMPLE / CT];
+        sample_keys<CT, M_SAMPLE>(sd, ks);
         if (FULL) load_chunk<IT, CT>(p, v);
         else load_chunk_ragged<IT, CT>(p, len, v);
-        window_from_keys<CT, M_SAMPLE_WIN>(sd, ks, *wl, &kl, &kh, &sh);
+        window_from_keys<CT, M_SAMPLE>(sd, ks, *wl, &kl, &kh, &sh);
         if (first && threadIdx.x == 0) { st->kl = kl; st->kh = kh; st->shift = sh; } /* for the select */
     } else {
         /* the window came from k_window; the stream loads go out first (the window words are
@@ -1796,13 +1796,18 @@ static inline unsigned grid_for(int64_t total) {
     return (unsigned)g;
 }
 
+static int collect_blocks(const SegTable& t) { return t.nblk * (CHUNK / (COLLECT_IT * COLLECT_THREADS * 4)); }
+static bool window_inline(const SegTable& t) { return collect_blocks(t) <= WINDOW_INLINE_MAX_BLOCKS; }
 void launch_window(const SegTable& t, SelHeader* head, hipStream_t s) {
-    if (!COLLECT_WINDOW_INLINE) hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, s, t, head);
+    if (!window_inline(t)) hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, s, t, head);
 }
 void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s) {
-    hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT, COLLECT_WINDOW_INLINE>),
-                       dim3(t.nblk * (CHUNK / (COLLECT_IT * COLLECT_THREADS * 4))), dim3(COLLECT_THREADS), 0, s, t,
-                       head, cand, res);
+    if (window_inline(t))
+        hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT, true>), dim3(collect_blocks(t)),
+                           dim3(COLLECT_THREADS), 0, s, t, head, cand, res);
+    else
+        hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT, false>), dim3(collect_blocks(t)),
+                           dim3(COLLECT_THREADS), 0, s, t, head, cand, res);
 }
 void launch_minprune(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
                      void* mp, uint32_t* tiecnt, hipStream_t s) {

@@ -57,7 +57,9 @@ constexpr int CHUNK = 16384;        /* elements per block in the streaming passe
 constexpr int STREAM_THREADS = 256; /* 64 elements = 16 float4 per thread          */
 constexpr int COLLECT_THREADS = 256; /* k_collect: 4 waves per block ...             */
 constexpr int COLLECT_IT = 16;       /* ... of 16 float4 per thread: one CHUNK        */
-constexpr bool COLLECT_WINDOW_INLINE = false; /* window per k_collect block, or one k_window launch */
+/* launch groups of at most this many k_collect blocks derive the window inside every block (one
+ * launch fewer: the launch-latency regime, e.g. cfg3); larger ones launch k_window once */
+constexpr int WINDOW_INLINE_MAX_BLOCKS = 32;
 constexpr int SEG_PER_LAUNCH = 24;
 constexpr int FB_GROUP = 12;          /* images per filter-bank level launch */
 
