@@ -168,6 +168,13 @@ int wtp_set_stage_events(void* const* events, int n);
  * Returns the previous mode (process-wide). */
 int wtp_set_resident(int mode);
 int wtp_resident_capacity(void); /* 0 if the current device cannot host the resident launch */
+/* Bound (microseconds) of every wait inside the resident launch; returns the previous bound.  A
+ * launch whose workgroups were not all resident at once times out there and stores NOTHING for
+ * the tensors concerned (inputs and outputs untouched): their records read path == 99
+ * (WTP_PATH_FAULT), and the caller re-runs exactly those tensors with wtp_set_resident(0).
+ * Default 200000; tests lower it to force the fault path. */
+unsigned wtp_set_resident_timeout_us(unsigned us);
+#define WTP_PATH_FAULT 99
 
 const char* wtp_last_error(void);
 int wtp_last_error_tensor(void); /* index of the tensor that failed validation, or -1 */

@@ -5,12 +5,13 @@
 #include <hip/hip_runtime.h>
 __device__ unsigned long long g_rprobe[256][20];
 __device__ unsigned long long g_cyc[256][2];
-__device__ unsigned long long g_sprobe[256][8];
+__device__ unsigned long long g_sprobe[256][16];
 #ifndef RESLAB_NOPROBE
 #define WTP_RPROBE(i) do { if (threadIdx.x == 0) { g_rprobe[blockIdx.x][i] = wall_clock64(); \
     if ((i) == 0) g_cyc[blockIdx.x][0] = __builtin_amdgcn_s_memtime(); \
     if ((i) == 7) g_cyc[blockIdx.x][1] = __builtin_amdgcn_s_memtime(); } } while (0)
 #define WTP_PROBE(i) do { if (threadIdx.x == 0) g_sprobe[blockIdx.x][i] = wall_clock64(); } while (0)
+#define WTP_PROBE_T(i, t) do { if (threadIdx.x == (t)) g_sprobe[blockIdx.x][i] = wall_clock64(); } while (0)
 #define WTP_WPROBE(i) WTP_RPROBE(12 + (i))
 #endif
 #include "../../wavelettransforms_amd/csrc/kernels.hip"
@@ -50,7 +51,7 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     std::vector<float> tms;
     unsigned long long pr[256][20];
-    std::vector<std::vector<double>> ph(18), sel(7);
+    std::vector<std::vector<double>> ph(18), sel(15);
     for (int r = 0; r < reps; ++r) {
         CK(hipEventRecord(a, 0));
         wtp_prune_layers_f32(ts.data(), 20, wid, 5, 50.0, ws, wsb, res, 0);
@@ -58,13 +59,13 @@ int main(int argc, char** argv) {
         CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b)); tms.push_back(ms * 1000);
         CK(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_rprobe), sizeof pr));
-        unsigned long long sp[256][8];
+        unsigned long long sp[256][16];
         CK(hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_sprobe), sizeof sp));
         int nb = 0; for (int t = 0; t < 20; ++t) { int64_t n = 1; for (int d = 0; d < 4; ++d) n *= shapes[t][d]; nb += (int)((n + RES_CHUNK - 1) / RES_CHUNK); }
         unsigned long long t0 = ~0ull;
         for (int i = 0; i < nb; ++i) t0 = std::min(t0, pr[i][0]);
         // per phase: median over workgroups of (probe_i - t0) in us (100 MHz clock)
-        for (int p = 0; p < 7; ++p) { /* select_body probes 0..6 */
+        for (int p = 0; p < 15; ++p) { /* select_body probes 0..14 */
             std::vector<double> v;
             for (int i = 0; i < nb; ++i) if (sp[i][p] >= t0) v.push_back((double)(sp[i][p] - t0) / 100.0);
             std::sort(v.begin(), v.end());
@@ -108,7 +109,7 @@ int main(int argc, char** argv) {
     std::sort(tms.begin(), tms.end());
     printf("k_resident cfg2: median %.2f us (min %.2f) per call, %.1f GB/s algorithmic\n", tms[tms.size() / 2], tms[0],
            8.0 * nw / (tms[tms.size() / 2] * 1e-6) / 1e9);
-    const char* names[18] = {"start", "window", "counted", "reserved", "scattered", "barrier", "selected", "stored",
+    const char* names[18] = {"start", "window", "counted", "hist-pub", "B1-arrive", "B1-pass", "selected", "stored",
                              "sampled", "spec-stored", "issued", "loaded", "w:cleared", "w:histo", "w:scanned",
                              "w:found", "sc:placed", "sc:issued"};
     for (int p = 0; p < 18; ++p) {
@@ -117,8 +118,9 @@ int main(int argc, char** argv) {
         std::sort(med.begin(), med.end()); std::sort(mx.begin(), mx.end());
         printf("  %-10s median WG %7.2f us   slowest WG %7.2f us\n", names[p], med[med.size() / 2], mx[mx.size() / 2]);
     }
-    const char* snames[7] = {"sel start", "counters", "bucket", "staged", "radix", "lerp", "published"};
-    for (int p = 0; p < 7; ++p) {
+    const char* snames[15] = {"-", "counters", "buckets", "B2-arrive", "B2-pass", "staged", "ranks", "-", "-", "-", "-", "-", "-", "-", "-"};
+    for (int p = 0; p < 15; ++p) {
+        if (p == 0 || p >= 7) continue;
         std::sort(sel[p].begin(), sel[p].end());
         printf("  select %-10s median WG %7.2f us\n", snames[p], sel[p][sel[p].size() / 2]);
     }

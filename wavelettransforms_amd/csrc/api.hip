@@ -424,6 +424,7 @@ int wtp_set_resident(int mode) {
     return prev;
 }
 int wtp_resident_capacity(void) { return resident_capacity(); }
+unsigned wtp_set_resident_timeout_us(unsigned us) { return set_resident_timeout_us(us); }
 
 size_t wtp_workspace_size(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level) {
     if (ntensors < 0 || (ntensors > 0 && !tensors)) return 0;

@@ -182,6 +182,9 @@ __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, i
 #ifndef WTP_PROBE
 #define WTP_PROBE(i)
 #endif
+#ifndef WTP_PROBE_T /* a probe taken by thread t */
+#define WTP_PROBE_T(i, t)
+#endif
 #ifndef WTP_CPROBE
 #define WTP_CPROBE(i)
 #endif
@@ -562,8 +565,10 @@ __device__ __forceinline__ void block_hist_select(const uint32_t* stage, int m, 
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     for (int i = tid; i < per * THREADS; i += THREADS) hist[i] = 0;
     __syncthreads();
+    WTP_PROBE_T(12, 0);
     for (int i = tid; i < m; i += THREADS) atomicAdd(&hist[stage[i] - lo], 1u);
     __syncthreads();
+    WTP_PROBE_T(13, 0);
     uint32_t c[HS_PER];
     uint32_t local = 0;
 #pragma unroll
@@ -574,6 +579,7 @@ __device__ __forceinline__ void block_hist_select(const uint32_t* stage, int m, 
     const uint32_t incl = wave_scan_u32(local);
     if (lane == 63) wt[wv] = incl;
     __syncthreads();
+    WTP_PROBE_T(14, 0);
     int cum = (int)(incl - local);
 #pragma unroll
     for (int i = 0; i < THREADS / 64; ++i) cum += i < wv ? (int)wt[i] : 0;
@@ -657,8 +663,7 @@ template <int THREADS, bool COH = false>
 __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st, const uint32_t* __restrict__ cand,
                              wtp_result* __restrict__ res, float* __restrict__ thr_out, uint32_t* stage,
                              int stage_cap, bool publish, uint32_t kl, uint32_t kh, uint32_t sh,
-                             int* path_out = nullptr, uint32_t* hscratch = nullptr, const ResRuns* rr = nullptr,
-                             bool prefer_wave = false) {
+                             int* path_out = nullptr, uint32_t* hscratch = nullptr, bool prefer_wave = false) {
     __shared__ int sbin[2];
     __shared__ int64_t sbefore[2];
     __shared__ uint32_t lsub[NSUB_MAX];
@@ -729,8 +734,10 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
     bool in_lds = false;
     bool full = ca == 0 || cb == 0 || s_ovf != 0;
     if (!full && (ca == 2 || cb == 2)) {
+        WTP_PROBE_T(8, 64);
         if (threadIdx.x >= 64 && threadIdx.x < 128) /* wave 1: both ranks from one scan */
             wave_find_buckets(lsub, nsub, ca == 2, ja, cb == 2, jb, sbin, sbefore);
+        WTP_PROBE_T(9, 64);
         __syncthreads();
         WTP_PROBE(2);
         blo = (ca == 2) ? sbin[0] : sbin[1];
@@ -739,44 +746,10 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
         /* adjacent ranks: buckets strictly between blo and bhi are empty */
         nlo = lsub[blo];
         nhi = (bhi != blo) ? lsub[bhi] : 0;
-        if (rr ? nlo + nhi > stage_cap : (nlo > bcap || nhi > bcap)) {
-            full = true;
-        } else if (rr) {
-            /* k_resident: bucket blo (then bhi) is spread over the runs of the segment's workgroups:
-             * one thread per (run, bucket) reads the run's two offsets, a block scan places the
-             * pieces, every thread copies its piece */
-            in_lds = true;
-            __shared__ uint32_t gwt[THREADS / 64];
-            const int t = threadIdx.x, nw = rr->nw;
-            const int nrun = bhi != blo ? 2 * nw : nw;
-            uint32_t cnt = 0;
-            const uint32_t* src = nullptr;
-            if (t < nrun) {
-                const int w = t < nw ? t : t - nw;
-                const int b = t < nw ? blo : bhi;
-                const uint32_t* run = rr->base + (int64_t)(rr->wb + w) * RES_WG_WORDS;
-                const uint32_t o0 = ldc<true>(run + b), o1 = ldc<true>(run + b + 1);
-                cnt = o1 - o0;
-                src = run + RES_OFF_WORDS + o0;
-            }
-            const uint32_t incl = wave_scan_u32(cnt);
-            if ((t & 63) == 63) gwt[t >> 6] = incl;
-            __syncthreads();
-            uint32_t dst = incl - cnt;
-            for (int w = 0; w < (t >> 6); ++w) dst += gwt[w];
-            for (uint32_t j0 = 0; j0 < cnt; j0 += 4) {
-                uint32_t kk[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) kk[q] = j0 + q < cnt ? ldc<true>(src + j0 + q) : 0u;
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (j0 + q < cnt) stage[dst + j0 + q] = kk[q];
-            }
-            __syncthreads();
-        }
+        if (nlo > bcap || nhi > bcap) full = true;
         if (!full) {
-            if (!rr) in_lds = nlo + nhi <= stage_cap;
-            if (in_lds && !rr) { /* STAGE_BATCH loads in flight per thread before any is used */
+            in_lds = nlo + nhi <= stage_cap;
+            if (in_lds) { /* STAGE_BATCH loads in flight per thread before any is used */
                 const int64_t m = nlo + nhi;
                 for (int64_t i0 = 0; i0 < m; i0 += (int64_t)THREADS * STAGE_BATCH) {
                     uint32_t v[STAGE_BATCH];
@@ -1094,93 +1067,172 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_mask_select(SegTable t, cons
  * also its output (in place) its workgroups meet at a segment-wide barrier before any writes.
  * Every wait is bounded (RES_TIMEOUT of the 100 MHz wall clock): a grid that is not co-resident
  * after all drains instead of hanging, and its records read MODE_FAULT. */
-constexpr uint64_t RES_TIMEOUT_TICKS = 20000000ull; /* 200 ms */
-constexpr int RES_STG = 32;                         /* inside keys a thread may stage (of its 96; ~11 expected) */
+/* The window search of k_resident for ONE wave over the flat NB-bin histogram h of the m sampled
+ * keys: lane l owns the RES_BPL consecutive bins from l * RES_BPL (odd stride: no bank
+ * conflicts); one scan of the lane sums finds the lane holding a sample rank, a second scan over
+ * that lane's bins (RES_BPL - 1 by the lanes, the last one by elimination) finds the bin. */
+constexpr int RES_BPL = 65;
+constexpr int RES_HBINS = 64 * RES_BPL; /* >= NB; the bins past NB stay 0 */
+static_assert(RES_HBINS >= NB, "flat window histogram");
+__device__ __forceinline__ void wave_find_bins_flat(const uint32_t* h, int ra, int rb, int* fa, int* fb) {
+    const int lane = threadIdx.x & 63;
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < RES_BPL; ++q) s += h[lane * RES_BPL + q];
+    const int incl = (int)wave_scan_u32(s), excl = incl - (int)s;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = i == 0 ? ra : rb;
+        int f = -1;
+        const uint64_t msk = __ballot(r >= 0 && excl <= r && r < incl);
+        if (msk) {
+            const int L = __ffsll((unsigned long long)msk) - 1;
+            const int before = __builtin_amdgcn_readlane(excl, L);
+            const uint32_t c = h[L * RES_BPL + lane];
+            const int i2 = before + (int)wave_scan_u32(lane < RES_BPL - 1 ? c : 0u);
+            const int e2 = i2 - (int)(lane < RES_BPL - 1 ? c : 0u);
+            const uint64_t m2 = __ballot(lane < RES_BPL - 1 && e2 <= r && r < i2);
+            f = L * RES_BPL + (m2 ? __ffsll((unsigned long long)m2) - 1 : RES_BPL - 1);
+        }
+        if (i == 0) *fa = f; else *fb = f;
+    }
+}
+__device__ __forceinline__ void window_search_flat(const SegDesc& sd, const uint32_t* h, int m, bool exact,
+                                                   uint32_t* kl_out, uint32_t* kh_out, uint32_t* sh_out, double sig,
+                                                   double add) {
+    const int64_t n = sd.n;
+    const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
+    int sa, sb;
+    if (exact) {
+        sa = (int)r0;
+        sb = (int)r1;
+    } else {
+        const double p = (double)r0 / (double)(n - 1);
+        const double s0 = p * (double)(m - 1), s1 = (double)r1 / (double)(n - 1) * (double)(m - 1);
+        const double d = sig * sqrt((double)m * p * (1.0 - p)) + add;
+        sa = (int)floor(s0 - d);
+        sb = (int)ceil(s1 + d);
+    }
+    int f0, f1;
+    wave_find_bins_flat(h, sa, sb < m ? sb : -1, &f0, &f1);
+    const uint32_t kl = (sa < 0 || f0 < 0) ? 0u : bin_lo_key(f0);
+    const uint32_t kh = (sb >= m || f1 < 0) ? 0xFFFFFFFFu : bin_hi_key(f1);
+    uint32_t sh = 0;
+    if (kh > kl + 1) {
+        const uint32_t R = kh - kl - 1;
+        const int bits = 32 - __clz(R);
+        sh = bits > sd.nsub_log2 ? bits - sd.nsub_log2 : 0;
+    }
+    *kl_out = kl;
+    *kh_out = kh;
+    *sh_out = sh;
+}
+
+constexpr uint32_t RES_POISON = 0x80000000u; /* a segment barrier counter whose wait timed out */
 
 __device__ __forceinline__ uint64_t wall_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
-/* Wave 0 waits until every shard counter has reached its expected arrivals (expect(lane));
- * block-uniform result: false on timeout. */
-template <class Expect>
-__device__ __forceinline__ bool res_wait(const uint32_t* ctr, int stride, const Expect& expect, int nctr) {
+/* Wait until the segment barrier counter reaches `want` arrivals (one lane polls with sc1 loads,
+ * s_sleep between polls; the other waves wait at the workgroup barrier, then load).  A wait that
+ * outlasts `timeout` ticks poisons the counter -- only while it is still short of `want`
+ * (compare-and-swap) -- so every workgroup of the segment either passes the barrier or sees the
+ * poison: all of them store, or none does.  Block-uniform result. */
+__device__ __forceinline__ bool res_wait(uint32_t* ctr, uint32_t want, uint64_t timeout) {
     __shared__ int s_ok;
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        const uint32_t want = lane < nctr ? expect(lane) : 0u;
+    if (threadIdx.x == 0) {
         const uint64_t t0 = wall_ticks();
-        bool ok = true;
+        int ok = 0;
         while (true) {
-            const uint32_t v = lane < nctr ? ldc<true>(ctr + lane * stride) : 0u;
-            if (__all(v >= want)) break;
-            if (wall_ticks() - t0 > RES_TIMEOUT_TICKS) { ok = false; break; }
+            const uint32_t v = ldc<true>(ctr);
+            if (v & RES_POISON) break;
+            if (v >= want) { ok = 1; break; }
+            if (wall_ticks() - t0 > timeout) {
+                if (atomicCAS(ctr, v, v | RES_POISON) == v) break;
+                continue; /* it moved: look again */
+            }
             __builtin_amdgcn_s_sleep(2);
         }
-        if (lane == 0) s_ok = ok;
+        s_ok = ok;
     }
     __syncthreads();
     return s_ok != 0;
 }
 
-template <bool FULL, bool SPEC>
+/* every wave drains its stores (vmcnt(0)), then lane 0 arrives: the sc1 hand-off form of
+ * MI355X_MICROARCH.md (one arrival per workgroup for all its stores) */
+__device__ __forceinline__ void res_arrive(uint32_t* ctr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(ctr, 1u);
+}
+
+template <bool FULL>
 __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, SelHeader* __restrict__ head, uint32_t q,
                                          uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
                                          float* __restrict__ thr_out, int64_t base, int len, uint32_t* raw,
-                                         uint32_t* lsub, uint32_t* lbase, uint32_t* loff, uint32_t (*wred)[8],
-                                         uint32_t* wstage) {
+                                         uint32_t* lsub, uint32_t (*wred)[8], uint32_t* wstage) {
     constexpr int CT = RES_THREADS, IT = RES_IT, NW = CT / 64;
     SelState* st = sel_region(head, q) + sd.slot;
     const bool first = base == 0;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    /* ---- P0: every thread loads its share of the sample and adds it to the LDS histogram;
-     * then wave 0 searches the histogram for the window while waves 1.. issue the chunk's loads
-     * (a wave stalls while its own 24 loads issue, so the search needs a wave of its own).  The
-     * sample loads go out before any chunk load, ahead of the stream in the memory queues. */
+    const uint64_t tmo = t.res_timeout;
     WTP_RPROBE(0);
     __shared__ uint32_t s_win[3];
     float4 v[IT];
+    /* ---- P0: the sample waves' loads go out before any chunk load of the workgroup (the barrier
+     * below orders them), then every wave issues its chunk; the sample arrives first (a wave's
+     * loads return in order) and is histogrammed while the chunk streams in; wave 0 searches the
+     * histogram for the window [kl, kh] bracketing the segment's two ranks */
     {
-        uint32_t ks[M_SAMPLE / CT];
-        sample_keys<CT, M_SAMPLE>(sd, ks);
-        for (int j = tid; j < NB + WCB; j += CT) raw[j] = 0u; /* fine bins, then the coarse bins */
+        uint32_t ks[RES_SPL];
+        const int64_t n = sd.n;
+        const bool exact = n <= RES_MS;
+        const int m = exact ? (int)n : RES_MS;
+        if (wv < RES_SW) {
+            const double step = exact ? 0.0 : (double)(n - SAMPLE_GROUP) / (double)(RES_MS / SAMPLE_GROUP - 1);
+#pragma unroll
+            for (int j = 0; j < RES_SPL; ++j) {
+                const int i = j * (64 * RES_SW) + tid;
+                const int64_t pos = exact ? min((int64_t)i, n - 1)
+                                          : (int64_t)((double)(i / SAMPLE_GROUP) * step) + (i % SAMPLE_GROUP);
+                ks[j] = abs_key(sd.data[pos]);
+            }
+        }
+        for (int j = tid; j < RES_HBINS; j += CT) raw[j] = 0u;
+        for (int j = tid; j < NSUB_MAX; j += CT) lsub[j] = 0u;
         if (first && tid == 0) { /* memory-side words: later adds come from other workgroups */
             stc(reinterpret_cast<unsigned long long*>(&res[sd.res].zero_count), 0ull);
             stc(&res[sd.res].path, 0);
         }
-        const int m = sd.n <= M_SAMPLE ? (int)sd.n : M_SAMPLE;
         __syncthreads();
         WTP_RPROBE(8);
+        if (FULL) load_chunk<IT, CT>(sd.data + base, v);
+        else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
+        WTP_RPROBE(10);
+        if (wv < RES_SW) {
 #pragma unroll
-        for (int j = 0; j < M_SAMPLE / CT; ++j)
-            if (j * CT + tid < m) {
-                const int b = key_bin(ks[j]);
-                atomicAdd(&raw[b], 1u);
-                atomicAdd(&raw[NB + (b >> 7)], 1u);
-            }
+            for (int j = 0; j < RES_SPL; ++j)
+                if (j * (64 * RES_SW) + tid < m) atomicAdd(&raw[key_bin(ks[j])], 1u);
+        }
         __syncthreads();
+        if (wv == 0) {
+            uint32_t wkl, wkh, wsh;
+            window_search_flat(sd, raw, m, exact, &wkl, &wkh, &wsh, t.pad[1] * 0.01, 8.0);
+            if (lane == 0) { s_win[0] = wkl; s_win[1] = wkh; s_win[2] = wsh; }
+            WTP_RPROBE(1);
+        }
     }
-    if (wv == 0) {
-        uint32_t wkl, wkh, wsh;
-        if (WTP_RES_ABL & 1) { wkl = 0x3c000000u; wkh = 0x3c800000u; wsh = 13; }
-        else window_search_wave<M_SAMPLE>(sd, raw, raw + NB, &wkl, &wkh, &wsh, t.pad[1] * 0.01, 8.0);
-        if (lane == 0) { s_win[0] = wkl; s_win[1] = wkh; s_win[2] = wsh; }
-        WTP_RPROBE(1);
-    }
-    if (FULL) load_chunk<IT, CT>(sd.data + base, v);
-    else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
-    WTP_RPROBE(10);
     __syncthreads();
     const uint32_t kl = s_win[0], kh = s_win[1], sh = s_win[2];
     /* ---- P1: one branch-free pass over the registers: counters, and the keys inside (kl, kh]
      * appended to the thread's own LDS column (slot j of thread t at col[j * CT]; every key is
      * written to the next free slot and kept only if inside -- no branch, no atomic).  Slots
      * past len were loaded as +0.0: never inside, and the block totals drop them once. */
-    const int nsub = 1 << sd.nsub_log2;
-    for (int i = tid; i < nsub; i += CT) lsub[i] = 0;
     const uint32_t span = kh - kl; /* >= 1 */
     uint32_t below = 0, eql = 0, mx = 0, cnt = 0;
     uint32_t* col = wstage + tid;
 #pragma unroll
-    for (int it = 0; it < ((WTP_RES_ABL & 2) ? 1 : IT); ++it) {
+    for (int it = 0; it < IT; ++it) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const uint32_t k = abs_key(opaque(f4_get(v[it], c)));
@@ -1194,16 +1246,16 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     }
     {
         const uint32_t r0 = wave_sum_u32(below), r1 = wave_sum_u32(eql), r2 = wave_max_u32(mx),
-                       r3 = wave_sum_u32(cnt), r4 = wave_max_u32(cnt);
-        if (lane == 0) { wred[wv][0] = r0; wred[wv][1] = r1; wred[wv][2] = r2; wred[wv][3] = r3; wred[wv][5] = r4; }
+                       r4 = wave_max_u32(cnt);
+        if (lane == 0) { wred[wv][0] = r0; wred[wv][1] = r1; wred[wv][2] = r2; wred[wv][5] = r4; }
     }
     __syncthreads();
     WTP_RPROBE(2);
-    uint32_t total = 0, wmax = 0;
+    uint32_t wmax = 0;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) { total += wred[w][3]; wmax = max(wmax, wred[w][5]); }
-    /* block-uniform: a thread's column or the block's sorted run overflowed -> the segment takes the full scan */
-    const bool ovf = wmax > (uint32_t)RES_STG || total > (uint32_t)RES_STAGE;
+    for (int w = 0; w < NW; ++w) wmax = max(wmax, wred[w][5]);
+    /* block-uniform: a thread's column overflowed -> the segment takes the full scan */
+    const bool ovf = wmax > (uint32_t)RES_STG;
     if (tid == 0) {
         unsigned long long a0 = 0, a1 = 0;
         uint32_t m2 = 0;
@@ -1216,152 +1268,285 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         atomicMax(&st->maxkey[sh8], m2);
         if (ovf) atomicOr(&st->overflow, 1u);
     }
-    /* bucket the staged keys into this workgroup's own run (no reservation round trip): an LDS
-     * histogram, its exclusive scan (the run's bucket offsets), a counting sort in LDS, then the
-     * offsets and the sorted keys written through (sc1) as whole lines; the segment's bucket
-     * totals are no-return atomic adds */
-    uint32_t* run = cand + (int64_t)blockIdx.x * RES_WG_WORDS; /* [offsets: NSUB_MAX + 1][keys: RES_STAGE] */
-    if (!(WTP_RES_ABL & 4) && !ovf) { /* block-uniform */
-        for (uint32_t j0 = 0; j0 < cnt; j0 += 4) { /* four column reads in flight per step */
-            uint32_t kk[4];
+    /* the inside keys' bucket histogram in LDS (eight column reads in flight per step), then the
+     * segment's bucket totals as no-return atomic adds */
+    if (!ovf) { /* block-uniform */
+        for (uint32_t j0 = 0; j0 < cnt; j0 += 8) {
+            uint32_t kk[8];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) kk[q] = j0 + q < cnt ? col[(j0 + q) * CT] : 0u;
+            for (int u = 0; u < 8; ++u) kk[u] = col[min(j0 + u, (uint32_t)RES_STG) * CT];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (j0 + q < cnt) atomicAdd(&lsub[(kk[q] - kl - 1u) >> sh], 1u);
+            for (int u = 0; u < 8; ++u)
+                if (j0 + u < cnt) atomicAdd(&lsub[(kk[u] - kl - 1u) >> sh], 1u);
         }
         __syncthreads();
-        constexpr int PER = NSUB_MAX / CT; /* consecutive buckets per thread */
-        static_assert(PER * CT == NSUB_MAX, "bucket split");
-        const int per = (nsub + CT - 1) / CT;
-        uint32_t cj[PER];
-        uint32_t lsum = 0;
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const int b = tid * per + j;
-            cj[j] = (j < per && b < nsub) ? lsub[b] : 0u;
-            lsum += cj[j];
-            if (cj[j]) atomicAdd(&st->sub[b], cj[j]);
-        }
-        const uint32_t incl = wave_scan_u32(lsum);
-        if (lane == 63) wred[wv][4] = incl;
-        __syncthreads();
-        uint32_t off = incl - lsum;
-        for (int w = 0; w < wv; ++w) off += wred[w][4];
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const int b = tid * per + j;
-            if (j < per && b < nsub) { loff[b] = off; stc(run + b, off); off += cj[j]; lsub[b] = 0; }
-        }
-        if (tid == 0) stc(run + nsub, total);
-        __syncthreads();
-        WTP_RPROBE(3);
-        uint32_t* sorted = raw; /* RES_STAGE keys; the window histogram is done with */
-        for (uint32_t j0 = 0; j0 < cnt; j0 += 4) { /* four reads, then four returning atomics, in flight */
-            uint32_t kk[4], at[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) kk[q] = j0 + q < cnt ? col[(j0 + q) * CT] : 0u;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                at[q] = j0 + q < cnt ? atomicAdd(&lsub[(kk[q] - kl - 1u) >> sh], 1u) : 0u;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (j0 + q < cnt) sorted[loff[(kk[q] - kl - 1u) >> sh] + at[q]] = kk[q];
-        }
-        __syncthreads();
-        WTP_RPROBE(16);
-        uint32_t* keys = run + RES_OFF_WORDS;
-        for (uint32_t i = tid; i < total; i += CT) stc(keys + i, sorted[i]);
-        WTP_RPROBE(17);
+        static_assert(NSUB_MAX == 2 * CT, "two buckets per thread");
+        const uint32_t c0 = lsub[2 * tid], c1 = lsub[2 * tid + 1];
+        if (c0) atomicAdd(&st->sub[2 * tid], c0);
+        if (c1) atomicAdd(&st->sub[2 * tid + 1], c1);
     }
-    /* ---- grid barrier (arrive) */
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    WTP_RPROBE(4);
+    WTP_RPROBE(3);
+    /* ---- segment barrier 1: every workgroup's counters and bucket totals are in */
     BarState* bar = bar_region(head, q);
-    const bool segbar = (t.pad[0] & RES_OPT_SEGBAR) != 0;
-    const uint32_t nwg_seg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
-    if (tid == 0) {
-        if (segbar) {
-            /* only the segment's workgroups meet; the last arrival of the grid flips the parity
-             * (every workgroup has read it by the time it arrives) */
-            atomicAdd(reinterpret_cast<uint32_t*>(&st->seg_bar[1]), 1u);
-            if (atomicAdd(&bar->arrive[0][0], 1u) == gridDim.x - 1u) stc(&head->parity, q ^ 1u);
-        } else {
-            atomicAdd(&bar->arrive[blockIdx.x & (NSHARD - 1)][0], 1u);
-        }
+    const uint32_t nwg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
+    uint32_t* b0 = reinterpret_cast<uint32_t*>(&st->seg_bar[0]);
+    uint32_t* b1 = reinterpret_cast<uint32_t*>(&st->seg_bar[1]);
+    uint32_t* b2 = reinterpret_cast<uint32_t*>(&st->seg_bar[2]);
+    res_arrive(b1);
+    /* the grid's last arrival flips the region parity (every workgroup has read it by then) */
+    if (tid == 0 && atomicAdd(&bar->arrive[0][0], 1u) == gridDim.x - 1u) stc(&head->parity, q ^ 1u);
+    WTP_RPROBE(4);
+    if (!res_wait(b1, nwg, tmo)) {
+        if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+        return; /* nothing stored: the caller's input and output are untouched */
     }
-    /* ---- speculative store while the other workgroups arrive: unless the window misses, every
-     * key < kl is below the threshold and every key > kh above it, so only keys in [kl, kh] are
-     * undecided -- write them unpruned now and fix the ones the threshold prunes after the
-     * select (in place, the input must stay intact for a possible full-scan select) */
-    float* qo = sd.out + base;
-    const bool spec = SPEC && sd.out != sd.data;
-    auto store_all = [&](auto&& g) {
-        if (FULL) {
-            float4* q4 = reinterpret_cast<float4*>(qo);
-#pragma unroll
-            for (int it = 0; it < IT; ++it) {
-                float4 y;
-                y.x = g(v[it].x); y.y = g(v[it].y); y.z = g(v[it].z); y.w = g(v[it].w);
-                q4[it * CT + tid] = y;
-            }
-        } else {
-            const __amdgpu_buffer_rsrc_t r = ragged_rsrc(qo, len);
-            const bool al = (sd.flags & SEG_ALIGNED) != 0;
-#pragma unroll
-            for (int it = 0; it < IT; ++it) {
-                float4 y;
-                y.x = g(v[it].x); y.y = g(v[it].y); y.z = g(v[it].z); y.w = g(v[it].w);
-                store4_tail(y, qo, r, it * CT + tid, len, al);
-            }
-        }
-    };
-    if (spec) store_all([&](float xv) { return abs_key(xv) < kl ? 0.0f : xv; });
-    WTP_RPROBE(9);
-    /* ---- grid barrier (wait) */
-    const int nblk = t.nblk;
-    bool ok = (WTP_RES_ABL & 16) ? true
-            : segbar ? res_wait(reinterpret_cast<const uint32_t*>(&st->seg_bar[1]), 0, [&](int) { return nwg_seg; }, 1)
-                     : res_wait(&bar->arrive[0][0], 32,
-                                [&](int s) { return (uint32_t)((nblk - s + NSHARD - 1) / NSHARD); }, NSHARD);
     WTP_RPROBE(5);
-    if (!segbar && blockIdx.x == 0 && tid == 0) head->parity = q ^ 1u; /* every workgroup has read it */
-    /* ---- P2 */
-    int path = 0;
-    const ResRuns rr{cand, sd.blk_begin, (int)((sd.n + RES_CHUNK - 1) / RES_CHUNK)};
-    const float thr = (WTP_RES_ABL & 8) ? __uint_as_float(kl)
-        : select_body<CT, true>(sd, st, cand, res, thr_out, raw, RES_STAGE, first, kl, kh, sh, &path, wstage, &rr,
-                                (t.pad[0] & RES_OPT_WSEL) != 0);
-    WTP_RPROBE(6);
-    if (path == MODE_FULL && !spec) { /* in place: nobody writes before the segment's scans end */
-        __syncthreads();
-        if (tid == 0) atomicAdd(&st->seg_bar[0], 1ull);
-        ok = res_wait(reinterpret_cast<const uint32_t*>(&st->seg_bar[0]), 0, [&](int) { return nwg_seg; }, 1) && ok;
+    /* ---- P2: the segment's counters and bucket totals in one round trip (every load in
+     * flight before any is used); a block scan of the totals names the bucket of each rank */
+    __shared__ unsigned long long s_cnt[2];
+    __shared__ uint32_t s_mk, s_ovf, s_wtot[NW];
+    __shared__ int s_bk[2];
+    __shared__ uint32_t s_bef[2], s_bn[2];
+    {
+        if (tid < 2) {
+            const unsigned long long* a = tid == 0 ? st->below : st->eq_lo;
+            unsigned long long x[NSHARD];
+#pragma unroll
+            for (int i = 0; i < NSHARD; ++i) x[i] = ldc<true>(a + i);
+            unsigned long long sum = 0;
+#pragma unroll
+            for (int i = 0; i < NSHARD; ++i) sum += x[i];
+            s_cnt[tid] = sum;
+        } else if (tid == 2) {
+            uint32_t x[NSHARD];
+#pragma unroll
+            for (int i = 0; i < NSHARD; ++i) x[i] = ldc<true>(st->maxkey + i);
+            uint32_t mm = 0;
+#pragma unroll
+            for (int i = 0; i < NSHARD; ++i) mm = max(mm, x[i]);
+            s_mk = mm;
+        } else if (tid == 3) {
+            s_ovf = ldc<true>(&st->overflow);
+        }
+        if (tid < 2) { s_bk[tid] = -1; s_bef[tid] = 0; s_bn[tid] = 0; }
     }
-    /* ---- P3: out = where(|x| < thr, 0, x) */
+    const uint32_t c0 = ldc<true>(st->sub + 2 * tid), c1 = ldc<true>(st->sub + 2 * tid + 1);
+    const uint32_t cs = c0 + c1;
+    const uint32_t incl = wave_scan_u32(cs);
+    if (lane == 63) s_wtot[wv] = incl;
+    __syncthreads();
+    WTP_PROBE(1);
+    const int64_t sbelow = (int64_t)s_cnt[0], seql = (int64_t)s_cnt[1];
+    const uint32_t mk = s_mk;
+    uint32_t excl = incl - cs, ninside = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) { const uint32_t x = s_wtot[w]; ninside += x; excl += w < wv ? x : 0u; }
+    const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
+    /* class of a rank: 0 outside the window, 1 == kl, 2 inside (kl, kh] at inside-rank j */
+    auto classify = [&](int64_t r, int64_t* j) {
+        if (r < sbelow) return 0;
+        r -= sbelow;
+        if (r < seql) return 1;
+        r -= seql;
+        if (r < (int64_t)ninside) { *j = r; return 2; }
+        return 0;
+    };
+    int64_t ja = 0, jb = 0;
+    const int ca = classify(r0, &ja), cb = classify(r1, &jb);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int64_t j = i == 0 ? ja : jb;
+        if ((i == 0 ? ca : cb) == 2 && j >= (int64_t)excl && j < (int64_t)(excl + cs)) {
+            const bool lo = j < (int64_t)(excl + c0);
+            s_bk[i] = 2 * tid + (lo ? 0 : 1);
+            s_bef[i] = lo ? excl : excl + c0;
+            s_bn[i] = lo ? c0 : c1;
+        }
+    }
+    __syncthreads();
+    WTP_PROBE(2);
+    bool full = ca == 0 || cb == 0 || s_ovf != 0;
+    int path = MODE_WINDOW;
+    uint32_t ka = kl, kb = kl;
+    uint32_t before = 0;
+    int m = 0;
+    uint32_t* stage = raw; /* the window histogram is done with */
+    if (!full && (ca == 2 || cb == 2)) {
+        const int ba = ca == 2 ? s_bk[0] : s_bk[1], bb = cb == 2 ? s_bk[1] : s_bk[0];
+        before = ca == 2 ? s_bef[0] : s_bef[1];
+        const uint32_t nlo = ca == 2 ? s_bn[0] : s_bn[1], nhi = (bb != ba) ? s_bn[1] : 0u;
+        m = (int)(nlo + nhi);
+        if (m > RES_SEL_MAX) {
+            full = true; /* uniform over the segment: the same totals everywhere */
+        } else {
+            /* ---- this workgroup's keys of buckets ba / bb into its slot (sc1 stores) */
+            __shared__ uint32_t s_fill;
+            if (tid == 0) s_fill = 0;
+            __syncthreads();
+            uint32_t* slot = cand + (int64_t)blockIdx.x * RES_SLOT_WORDS;
+            for (uint32_t j0 = 0; j0 < cnt; j0 += 8) {
+                uint32_t kk[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) kk[u] = col[min(j0 + u, (uint32_t)RES_STG) * CT];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int bk = (int)((kk[u] - kl - 1u) >> sh);
+                    if (j0 + u < cnt && (bk == ba || bk == bb)) {
+                        const uint32_t p = atomicAdd(&s_fill, 1u);
+                        if (p < (uint32_t)RES_SLOT_CAP) stc(slot + 1 + p, kk[u]);
+                    }
+                }
+            }
+            __syncthreads();
+            if (tid == 0) stc(slot, s_fill);
+            /* ---- segment barrier 2: every slot of the segment is written */
+            res_arrive(b2);
+            WTP_PROBE(3);
+            if (!res_wait(b2, nwg, tmo)) {
+                if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+                return;
+            }
+            WTP_PROBE(4);
+            /* ---- the segment's slots (consecutive in the candidate region) in one round trip
+             * per four words a thread, copied raw into LDS (the columns are done with) */
+            const int wb = sd.blk_begin;
+            const int nwords = (int)nwg * RES_SLOT_WORDS;
+            const uint32_t* sl = cand + (int64_t)wb * RES_SLOT_WORDS;
+            uint32_t* rawsl = wstage;
+            for (int i0 = tid; i0 < nwords; i0 += 4 * CT) {
+                uint32_t kv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) kv[u] = i0 + u * CT < nwords ? ldc<true>(sl + i0 + u * CT) : 0u;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (i0 + u * CT < nwords) rawsl[i0 + u * CT] = kv[u];
+            }
+            __syncthreads();
+            __shared__ uint32_t s_so[RES_MAX_WG];
+            __shared__ uint32_t s_tot, s_sovf;
+            if (wv == 0) { /* exclusive scan of the slot counts, four slots per lane */
+                uint32_t c4[RES_MAX_WG / 64], s4 = 0, o4 = 0;
+#pragma unroll
+                for (int u = 0; u < RES_MAX_WG / 64; ++u) {
+                    const int w = 4 * lane + u;
+                    c4[u] = w < (int)nwg ? rawsl[w * RES_SLOT_WORDS] : 0u;
+                    o4 |= c4[u] > (uint32_t)RES_SLOT_CAP ? 1u : 0u;
+                    s4 += c4[u];
+                }
+                const uint32_t inc4 = wave_scan_u32(s4);
+                uint32_t o = inc4 - s4;
+#pragma unroll
+                for (int u = 0; u < RES_MAX_WG / 64; ++u) {
+                    const int w = 4 * lane + u;
+                    if (w < (int)nwg) s_so[w] = o;
+                    o += c4[u];
+                }
+                const uint64_t ob = __ballot(o4 != 0);
+                if (lane == 63) s_tot = inc4;
+                if (lane == 0) s_sovf = ob != 0;
+            }
+            __syncthreads();
+            if (s_sovf || (int)s_tot != m) {
+                full = true; /* a slot overflowed: uniform over the segment (same slots everywhere) */
+            } else {
+                for (int i = tid; i < nwords; i += CT) {
+                    const int w = i / RES_SLOT_WORDS, j = i % RES_SLOT_WORDS;
+                    if (j >= 1 && (uint32_t)j <= rawsl[w * RES_SLOT_WORDS]) stage[s_so[w] + j - 1] = rawsl[i];
+                }
+                __syncthreads();
+                WTP_PROBE(5);
+                /* ---- the ranks among the staged keys (buckets ba..bb; buckets between are empty:
+                 * the two ranks are adjacent): an LDS radix select of both at once */
+                const uint32_t lo = (uint32_t)((uint64_t)kl + 1 + ((uint64_t)ba << sh));
+                const uint32_t hi = (uint32_t)min((uint64_t)kh, (uint64_t)kl + ((uint64_t)(bb + 1) << sh));
+                uint32_t xa = kl, xb = kl;
+                select_in_range<CT>([&](int64_t i) { return stage[i]; }, [](uint32_t) { return true; }, (int64_t)m, lo,
+                                    hi, ja - (int64_t)before, jb - (int64_t)before, ca == 2, cb == 2, &xa, &xb);
+                ka = ca == 2 ? xa : kl;
+                kb = cb == 2 ? xb : kl;
+                path = MODE_CAND;
+            }
+        }
+    }
+    WTP_PROBE(6);
+    if (full) {
+        /* the window missed (or a column or slot overflowed): exact radix select over the
+         * segment's input in memory -- every workgroup of the segment takes this branch */
+        const float* x = sd.data;
+        select_in_range<CT>([&](int64_t i) { return abs_key(x[i]); }, [](uint32_t) { return true; }, sd.n, 0u,
+                            0xFFFFFFFFu, r0, r1, true, true, &ka, &kb);
+        path = MODE_FULL;
+    }
+    /* threshold: numpy/lib/function_base.py _lerp -- diff in float32, the blend in float64 */
+    const float fa = __uint_as_float(ka), fb = __uint_as_float(kb);
+    const float diff = fb - fa;
+    const double g = sd.gamma;
+    double thr64 = (g >= 0.5) ? (double)fb - (double)diff * (1.0 - g) : (double)fa + (double)diff * g;
+    if (mk > 0x7F800000u) thr64 = __longlong_as_double(0x7FF8000000000000ll); /* NaN present: np.percentile is NaN */
+    const float thr = (float)thr64;
+    const bool nan = thr != thr; /* also inf - inf inside the lerp */
+    if (first) {
+        /* zeros of where(|x| < thr, 0, x) = #(key < tk), tk = bits(thr) when thr > 0, else 1 (only
+         * the zeros themselves); ka <= thr <= kb and the ranks are adjacent, so #(key < tk) =
+         * below + [tk > kl] eq + before + #(staged < tk).  A NaN threshold prunes nothing: every
+         * workgroup counts the zeros of its copy below. */
+        unsigned long long zc = 0;
+        if (!nan) {
+            const uint32_t tk = thr > 0.0f ? __float_as_uint(thr) : 1u;
+            if (path == MODE_FULL) {
+                zc = (unsigned long long)block_count_below<CT>([&](int64_t i) { return abs_key(sd.data[i]); }, sd.n, tk);
+            } else {
+                uint32_t c = 0;
+                if (path == MODE_CAND)
+                    for (int i = tid; i < m; i += CT) c += stage[i] < tk;
+                const unsigned long long sc = block_sum_u64<CT>(c);
+                zc = (unsigned long long)sbelow + (tk > kl ? (unsigned long long)seql : 0ull) +
+                     (path == MODE_CAND ? (unsigned long long)before : 0ull) + sc;
+            }
+        }
+        if (tid == 0) {
+            thr_out[sd.res] = thr; /* per tensor */
+            wtp_result& r = res[sd.res];
+            r.numel = sd.numel;
+            r.coeff_numel = sd.n;
+            if (zc) atomicAdd((unsigned long long*)&r.zero_count, zc);
+            r.thr64 = thr64;
+            r.thr32_bits = __float_as_uint(thr);
+            r.max_abs_bits = mk;
+            r.eff_level = sd.eff_level;
+            atomicMax(&r.path, path);
+        }
+    }
+    if (path == MODE_FULL && sd.out == sd.data) { /* in place: nobody writes before the segment's scans end */
+        res_arrive(b0);
+        if (!res_wait(b0, nwg, tmo)) {
+            if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+            return;
+        }
+    }
+    WTP_RPROBE(6);
+    /* ---- P3: out = where(|x| < thr, 0, x) from registers (a NaN threshold prunes nothing) */
+    float* qo = sd.out + base;
     auto fin = [&](float xv) { return (fabsf(xv) < thr) ? 0.0f : xv; };
-    if (!spec || path == MODE_FULL || thr != thr) {
-        store_all(fin); /* uniform: everything (a NaN threshold prunes nothing) */
-    } else {
-        /* only the float4s holding a key in [kl, kh] that the threshold prunes */
+    if (FULL) {
+        float4* q4 = reinterpret_cast<float4*>(qo);
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            bool fix = false;
+            float4 y;
+            y.x = fin(v[it].x); y.y = fin(v[it].y); y.z = fin(v[it].z); y.w = fin(v[it].w);
+            q4[it * CT + tid] = y;
+        }
+    } else {
+        const __amdgpu_buffer_rsrc_t rr = ragged_rsrc(qo, len);
+        const bool al = (sd.flags & SEG_ALIGNED) != 0;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float xv = f4_get(v[it], c);
-                fix = fix || (abs_key(xv) >= kl && fabsf(xv) < thr);
-            }
-            if (fix) {
-                float4 y;
-                y.x = fin(v[it].x); y.y = fin(v[it].y); y.z = fin(v[it].z); y.w = fin(v[it].w);
-                if (FULL) reinterpret_cast<float4*>(qo)[it * CT + tid] = y;
-                else store4_tail(y, qo, ragged_rsrc(qo, len), it * CT + tid, len, (sd.flags & SEG_ALIGNED) != 0);
-            }
+        for (int it = 0; it < IT; ++it) {
+            float4 y;
+            y.x = fin(v[it].x); y.y = fin(v[it].y); y.z = fin(v[it].z); y.w = fin(v[it].w);
+            store4_tail(y, qo, rr, it * CT + tid, len, al);
         }
     }
-    if (thr != thr) { /* uniform: the copy's zeros are counted (the pad slots read as +0.0 excluded) */
+    if (nan) { /* uniform: the copy's zeros are counted (the pad slots read as +0.0 excluded) */
         uint32_t z = 0;
 #pragma unroll
         for (int it = 0; it < IT; ++it)
@@ -1370,19 +1555,15 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         const unsigned long long tot = block_sum_u64<CT>(z) - (unsigned long long)(RES_CHUNK - len);
         if (tid == 0 && tot) atomicAdd((unsigned long long*)&res[sd.res].zero_count, tot);
     }
-    if (!ok && tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
     WTP_RPROBE(7);
 }
 
-template <bool SPEC>
 __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader* __restrict__ head,
                                                           uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
                                                           float* __restrict__ thr_out) {
-    constexpr size_t RAW = sizeof(WindowLds<RES_THREADS>) > RES_STAGE * 4 ? sizeof(WindowLds<RES_THREADS>) : RES_STAGE * 4;
-    __shared__ __attribute__((aligned(16))) uint32_t raw[RAW / 4]; /* P0 window histogram, then P2 stage */
-    __shared__ uint32_t lsub[NSUB_MAX], lbase[NSUB_MAX];
+    __shared__ __attribute__((aligned(16))) uint32_t raw[RES_HBINS > RES_SEL_MAX ? RES_HBINS : RES_SEL_MAX];
+    __shared__ uint32_t lsub[NSUB_MAX];
     __shared__ uint32_t wred[RES_THREADS / 64][8];
-    __shared__ uint32_t loff[NSUB_MAX];
     __shared__ uint32_t wstage[(RES_STG + 1) * RES_THREADS]; /* 66 KB: RES_STG slots + the discard slot per thread */
     const uint32_t q = head->parity;
     {   /* clear this workgroup's slice of the idle region (the previous launch's) */
@@ -1399,9 +1580,9 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader*
     const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * RES_CHUNK;
     const int len = (int)min((int64_t)RES_CHUNK, sd.n - base);
     if ((sd.flags & SEG_ALIGNED) && len == RES_CHUNK)
-        res_body<true, SPEC>(t, sd, head, q, cand, res, thr_out, base, len, raw, lsub, lbase, loff, wred, wstage);
+        res_body<true>(t, sd, head, q, cand, res, thr_out, base, len, raw, lsub, wred, wstage);
     else
-        res_body<false, SPEC>(t, sd, head, q, cand, res, thr_out, base, len, raw, lsub, lbase, loff, wred, wstage);
+        res_body<false>(t, sd, head, q, cand, res, thr_out, base, len, raw, lsub, wred, wstage);
 }
 
 /* The in-place segments whose k_mask_select took the full-scan select: the mask pass that
@@ -1835,24 +2016,22 @@ int resident_capacity() {
     }
     int per = 0, cus = 0;
     int cap = -1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_resident<true>, RES_THREADS, 0) == hipSuccess &&
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_resident, RES_THREADS, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && per >= 1 && cus > 0)
         cap = cus; /* one workgroup per CU: the form the inter-workgroup hand-off is specified for */
     (void)hipGetLastError();
     if (dev < 16) cache[dev].store(cap, std::memory_order_relaxed);
     return cap > 0 ? cap : 0;
 }
+static std::atomic<uint32_t> g_res_timeout_us{RES_TIMEOUT_DEFAULT_US};
+uint32_t set_resident_timeout_us(uint32_t us) { return g_res_timeout_us.exchange(us); }
 void launch_resident(const SegTable& t0, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
                      hipStream_t s) {
-    static const int spec = [] { const char* e = getenv("WTP_RES_SPEC"); return e ? atoi(e) : 0; }();
-    static const int opts = [] { const char* e = getenv("WTP_RES_OPTS"); return e ? atoi(e) : RES_OPT_DEFAULT; }();
     static const int sig = [] { const char* e = getenv("WTP_RES_SIGMA"); return e && atoi(e) > 0 ? atoi(e) : RES_SIGMA_X100; }();
     SegTable t = t0;
-    t.pad[0] = opts;
-    const int grid = t.nblk;
     t.pad[1] = sig; /* window margin: sig/100 binomial sigma + 8 sample ranks */
-    if (spec) hipLaunchKernelGGL(k_resident<true>, dim3(grid), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
-    else hipLaunchKernelGGL(k_resident<false>, dim3(grid), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
+    t.res_timeout = g_res_timeout_us.load(std::memory_order_relaxed) * 100u; /* 100 MHz wall clock */
+    hipLaunchKernelGGL(k_resident, dim3(t.nblk), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
 }
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
                      hipStream_t s) {

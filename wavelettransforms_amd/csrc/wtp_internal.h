@@ -93,6 +93,8 @@ struct SegTable {
     int32_t nseg;
     int32_t nblk;
     int32_t pad[2];
+    uint32_t res_timeout; /* k_resident: bound of every wait, in ticks of the 100 MHz wall clock */
+    int32_t pad2;
     int32_t blk_begin[SEG_PER_LAUNCH]; /* INT32_MAX past nseg: block -> segment in one scalar sweep */
     SegDesc s[SEG_PER_LAUNCH];
 };
@@ -167,22 +169,34 @@ void launch_mask_inplace(const SegTable& t, const wtp_result* res, const float* 
 constexpr int RES_THREADS = 512;
 constexpr int RES_IT = 24;                          /* float4 per thread held in VGPRs */
 constexpr int RES_CHUNK = RES_THREADS * RES_IT * 4; /* 49152 elements per workgroup   */
-constexpr int RES_OPT_SEGBAR = 1;                   /* segment-wide barriers instead of the grid barrier */
-constexpr int RES_OPT_WSEL = 2;                     /* one wave per rank for <= 1024 staged keys */
-constexpr int RES_OPT_DEFAULT = RES_OPT_SEGBAR;
+#ifndef WTP_RES_MS
+#define WTP_RES_MS 4096
+#endif
+#ifndef WTP_RES_SW
+#define WTP_RES_SW 4
+#endif
+/* k_resident's window sample: RES_MS keys per segment, loaded by the first RES_SW waves of every
+ * workgroup (RES_SPL per lane) ahead of the chunk's loads */
+constexpr int RES_MS = WTP_RES_MS;
+constexpr int RES_SW = WTP_RES_SW;
+constexpr int RES_SPL = RES_MS / (64 * RES_SW);
+/* a wave may have at most 63 vector-memory instructions outstanding: the sample's loads and
+ * the chunk's must all be in flight together */
+static_assert(RES_SPL + RES_IT <= 63 && RES_SPL * 64 * RES_SW == RES_MS, "k_resident sample geometry");
 /* k_resident's window margin in binomial sigmas x 100 (+ 8 sample ranks): a miss costs a full
  * scan of the segment, 4 sigma makes that ~1e-4 per segment; the three-launch form keeps 6 + 24 */
 constexpr int RES_SIGMA_X100 = 400;
 constexpr int RES_MAX_WG = 256;                     /* workgroups a resident launch may hold (<= CUs) */
-constexpr int RES_STAGE = 12288;                    /* inside keys a workgroup may keep (its sorted run) */
-constexpr int RES_OFF_WORDS = NSUB_MAX + 32;        /* a run's bucket offsets (+ total), padded to whole lines */
-constexpr int RES_WG_WORDS = RES_OFF_WORDS + RES_STAGE; /* one workgroup's run in the candidate region */
-/* the runs of one segment for the select: workgroups [wb, wb + nw) of the launch */
-struct ResRuns {
-    const uint32_t* base;
-    int wb, nw;
-};
-int resident_capacity();                            /* co-resident workgroups on the current device */
+constexpr int RES_STG = 32;                         /* inside keys a thread may stage (of its 96; ~11 expected) */
+/* After the first segment barrier every workgroup publishes the keys of the (one or two)
+ * buckets holding the segment's ranks in a slot of its own: word 0 the count, then the keys */
+constexpr int RES_SLOT_WORDS = 32;
+constexpr int RES_SLOT_CAP = RES_SLOT_WORDS - 1;
+constexpr int RES_WG_WORDS = RES_SLOT_WORDS;        /* one workgroup's slot in the candidate region */
+constexpr int RES_SEL_MAX = 1024;                   /* keys the one-wave select takes (more: full scan) */
+constexpr uint32_t RES_TIMEOUT_DEFAULT_US = 200000; /* a wait this long means the grid is not co-resident */
+int resident_capacity();
+uint32_t set_resident_timeout_us(uint32_t us); /* every k_resident wait's bound; returns the previous one */                            /* co-resident workgroups on the current device */
 void launch_resident(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
                      hipStream_t s);
 /* min-weight pruning after window + collect: mp = 16 B per tensor, tiecnt = one u32 per
