@@ -1,37 +1,48 @@
 #!/usr/bin/env python3
 """bench.py -- headline benchmark of the DWT -> percentile-threshold -> IDWT path on MI355X.
 
-Workload (BASELINE.json configs[1]): bior3.3, level 5, 50th percentile
-over the 20 Conv2d weights of ResNet-18 (11,166,912 fp32 weight coefficients per step;
-synthetic kaiming-scaled values from csrc/wt_synth.h, generated on the device, resident in HBM
-before the timed region).  One step = one wavelet_pruning-equivalent launch sequence over the
-whole state_dict (every layer its own level/percentile, as dwt_pruning.py:130-174 does).
-Multi-GPU (torchrun, one process per GPU): weak scaling, every rank prunes its own model
-replica (independent objects, no data-path collective); the cfg4 variant (ONE model's layers
-LPT-sharded + one RCCL all-gather) is measured as an extra leg and reported beside it.
+Workload (BASELINE.json configs[1]): bior3.3, level 5, 50th percentile over
+the 20 Conv2d weights of ResNet-18 (11,166,912 fp32 weight coefficients per model; synthetic
+kaiming-scaled values from csrc/wt_synth.h, generated on the device, resident in HBM before the
+timed region).  One step = one wavelet_pruning-equivalent pass over the whole state_dict (every
+layer its own level and percentile, dwt_pruning.py:130-174).
 
-Prints ONE JSON line on rank 0 (the driver contract).  --config cfg3/cfg5 run the other
-single-GPU configs for DESIGN.md; they are not the headline line.
+--gpus N (N > 1): unless WORLD_SIZE is set (torchrun), N rank processes are started here, before
+anything touches the GPU (python -m torch.distributed.run on 127.0.0.1), one per GPU.  The
+headline at N > 1 is north_star's split, BASELINE configs[3] (cfg4): ONE model's layers
+LPT-sharded over the ranks, each rank pruning its layers straight into its flat shard, then ONE
+RCCL all_gather_into_tensor that reassembles the pruned state_dict on every rank -- strong
+scaling of one model (end-to-end per step = compute + all-gather, max over ranks).  The replica
+leg (every rank prunes its own model, no collective: weak scaling) is reported beside it.
+--config cfg5 (BASELINE configs[4]): 64 blocks of 4096^2 (db8 level 5) split over the ranks
+(strong scaling); --config cfg3 the MLP (launch-latency regime).
+
+Prints ONE JSON line on rank 0 (the driver contract).
 """
 import argparse
 import ctypes
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_NOFMA_TFLOPS = 78.6   # FP32 vector peak without FMA contraction
 METRIC = "weight-coeffs/s for L5 bior3.3 DWT+thresh+IDWT; achieved HBM GB/s vs peak"
 STAGES = ["forward_dwt", "k_window", "k_collect", "k_mask_select", "inverse_dwt"]
 KERNEL_OF_STAGE = {"k_window": "k_window", "k_collect": "k_collect_t", "k_mask_select": "k_mask_select",
                    "forward_dwt": "k_fwd_level", "inverse_dwt": "k_inv_level"}
-DWT_STAGES = ("forward_dwt", "inverse_dwt")  # one level launch per level: stage bytes = levels x per launch
+DWT_STAGES = ("forward_dwt", "inverse_dwt")
+CFG5_BLOCKS = 64
+DB8_L5_FLOP_PER_ELEM = 170.5  # 4 F sum_k 4^-k MACs, no FMA, F = 16, L = 5
 
 
 def parse():
@@ -40,87 +51,226 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg5"])
-    ap.add_argument("--blocks", type=int, default=8, help="cfg5: 4096^2 blocks per GPU")
+    ap.add_argument("--blocks", type=int, default=CFG5_BLOCKS, help="cfg5: 4096^2 blocks in all (split over ranks)")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps captured per hipGraph replay")
-    ap.add_argument("--stage-reps", type=int, default=30)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--replays", type=int, default=60, help="graph replays timed one by one (p10/p50/p90)")
+    ap.add_argument("--stamp-reps", type=int, default=50, help="launches timed by in-kernel stamps")
+    ap.add_argument("--stage-reps", type=int, default=20)
+    ap.add_argument("--cold-reps", type=int, default=30)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--cold", action="store_true", help="also time with the Infinity Cache flushed")
+    ap.add_argument("--no-cold", action="store_true")
     ap.add_argument("--flatten", action="store_true",
                     help="the 1-D flattened mode (WTP_FLATTEN; an extension, not the headline path)")
     ap.add_argument("--no-resident", action="store_true",
                     help="level-0 groups in the three-launch form instead of the one-launch k_resident")
+    ap.add_argument("--no-rocprof", action="store_true", help="skip the in-run rocprofv3 kernel-stats child")
+    ap.add_argument("--profile-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
-def workload(cfg, rank, blocks):
-    from wavelettransforms_amd import workloads as W
-    if cfg == "cfg2":
-        ts = [(n, s, seed + 1000 * rank, tid, e) for (n, s, seed, tid, e) in W.resnet18_tensors(0)]
-        return "resnet18_conv_state_dict", "bior3.3", 5, 50.0, ts
-    if cfg == "cfg3":
-        return "mnist_mlp_linear", "rbio2.2", 3, 50.0, W.mlp_tensors(3)
-    ts = W.block_tensors(blocks * (rank + 1))[blocks * rank:]
-    return "synthetic_4096x4096_blocks", "db8", 5, 50.0, ts
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-def stage_bytes(stage, n_w, pop, has_dwt):
-    """Algorithmic bytes each stage must move (4 B read of w + 4 B write of w')."""
-    if stage in ("forward_dwt", "inverse_dwt") and not has_dwt:
-        return 0
-    return {"forward_dwt": 4 * n_w + 4 * pop, "k_window": 0, "k_collect": 4 * pop,
-            "k_mask_select": 8 * n_w if pop == n_w else 0, "inverse_dwt": 4 * pop + 4 * n_w}[stage]
+def launch_ranks(n):
+    """Start n rank processes (one per GPU) and relay their exit status.  Runs before this process
+    touches the GPU: the ranks are children, nothing is exec'ed over a GPU-initialised process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def pmc_traffic(config, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summaries
-    (profiles/pmc_<config>*.json, FETCH_SIZE x2 + WRITE_SIZE per DESIGN.md), if present."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_%s*.json" % config))):
-        try:
-            with open(path) as fh:
-                d = json.load(fh)
-            return d["kernels"][kernel]["hbm_bytes_per_launch"]
-        except Exception:
-            continue
-    return None
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this config's
+    current kernels (profiles/pmc_<config>.json: 2 x FETCH_SIZE + WRITE_SIZE, separate passes)."""
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % config)
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d["kernels"][kernel]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT), d.get("source")
+    except Exception:
+        return None, None, None
+
+
+def rocprof_child(args, timeout=240):
+    """The headline step loop of this very configuration under rocprofv3 --kernel-trace --stats,
+    run as a child process BEFORE this process touches the GPU; returns {kernel name: (calls,
+    average ns)} from its kernel-stats summary, or None if the profiler is unavailable."""
+    import csv
+    import shutil
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    d = tempfile.mkdtemp(prefix="wtp_bench_prof_", dir="/tmp")
+    cmd = [prof, "--kernel-trace", "--stats", "-d", d, "-o", "run", "--output-format", "csv", "--",
+           sys.executable, os.path.abspath(__file__), "--profile-child", "--config", args.config,
+           "--steps", str(max(args.steps, 200)), "--warmup", str(args.warmup), "--blocks", str(args.blocks)]
+    if args.flatten:
+        cmd.append("--flatten")
+    if args.no_resident:
+        cmd.append("--no-resident")
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                       timeout=timeout, check=True)
+        stats = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+        out = {}
+        with open(stats[0]) as fh:
+            for row in csv.DictReader(fh):
+                out[row["Name"]] = (int(row["Calls"]), float(row["TotalDurationNs"]))
+        return out
+    except Exception:
+        return None
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def rocprof_avg_us(stats, kernel):
+    """Average duration (us) over every launch of the wtp kernel named `kernel` (any template
+    instance) in a rocprof_child summary; (None, 0) if absent."""
+    calls, total = 0, 0.0
+    for name, (c, t) in (stats or {}).items():
+        base = name.split("(")[0].split("<")[0].replace("void ", "").strip()
+        if base == "wtp::" + kernel:
+            calls += c
+            total += t
+    return (total / calls * 1e-3, calls) if calls else (None, 0)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        n = min(n, int(omp))  # the box's CPU share (16 per GPU there)
+    return max(1, n)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    # single process: first the kernel-stats child (rocprofv3 over this same step loop), before
+    # this process touches the GPU; its per-kernel average is the roofline's launch duration
+    prof_stats = None
+    if (not args.profile_child and not args.no_rocprof and int(os.environ.get("WORLD_SIZE", "1")) == 1):
+        prof_stats = rocprof_child(args)
+
+    import torch
+    import torch.distributed as dist
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # WTP_BENCH_REHEARSAL=1: the N > 1 code path on a one-GPU box (every rank on device 0, gloo
+    # instead of RCCL) -- a functional rehearsal only, its numbers mean nothing
+    rehearsal = os.environ.get("WTP_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from wavelettransforms_amd import _native as N
     from wavelettransforms_amd import engine
+    from wavelettransforms_amd import workloads as W
+    from wavelettransforms_amd.sharding import REC_BYTES, ShardPlan, _Shard, assemble
 
+    L = N.lib()
     if args.no_resident:
         engine.set_resident(False)
-    name, wavelet, level, pct, ts = workload(args.config, rank, args.blocks)
-    xs = [engine.synth(s, seed, tid, e, device=dev) for (_, s, seed, tid, e) in ts]
-    outs = [torch.empty_like(x) for x in xs]
-    n_w = sum(x.numel() for x in xs)
 
-    def step():
-        return engine.launch(xs, wavelet, level, pct, outs=outs, carry_level=False, flatten=args.flatten)
+    # ---------------------------------------------------------------- workload
+    if args.config == "cfg2":
+        name, wavelet, level, pct = "resnet18_conv_state_dict", "bior3.3", 5, 50.0
+        model = [(s, seed, tid, e) for (_, s, seed, tid, e) in W.resnet18_tensors(0)]
+    elif args.config == "cfg3":
+        name, wavelet, level, pct = "mnist_mlp_linear", "rbio2.2", 3, 50.0
+        model = [(s, seed, tid, e) for (_, s, seed, tid, e) in W.mlp_tensors(3)]
+    else:
+        name, wavelet, level, pct = "synthetic_4096x4096_blocks", "db8", 5, 50.0
+        nb = max(world, args.blocks)
+        per = nb // world
+        model = [(s, seed, tid, e) for (_, s, seed, tid, e) in W.block_tensors(per * world)]
+    sharded = world > 1 and args.config in ("cfg2", "cfg3")   # cfg4: one model over the ranks
+    if args.config == "cfg5":
+        mine = model[rank * per:(rank + 1) * per]               # cfg5: the blocks split over the ranks
+    elif sharded:
+        plan = ShardPlan([s for (s, *_) in model], world)
+        mine = [model[i] for i in plan.mine[rank]]
+    else:
+        mine = model
+    xs_all = [engine.synth(s, seed, tid, e, device=dev) for (s, seed, tid, e) in
+              (model if sharded else mine)]
+    n_model = sum(int(np.prod(s)) for (s, *_) in model)          # weights of the whole job per step
+    n_w = sum(x.numel() for x in (xs_all if not sharded else [xs_all[i] for i in plan.mine[rank]]))
+
+    if sharded:
+        shard = _Shard(xs_all, plan, rank, dev)
+        gathered = torch.empty(world * plan.slice, dtype=torch.float32, device=dev)
+
+        def compute():
+            if shard.mine:
+                shard.run(shard.mine, wavelet, level, pct)
+
+        def gather():
+            dist.all_gather_into_tensor(gathered, shard.buf)
+
+        def step():
+            compute()
+            gather()
+        xs = [xs_all[i] for i in plan.mine[rank]]
+    else:
+        xs = xs_all
+        outs = [torch.empty_like(x) for x in xs]
+        res_buf = torch.empty(max(1, len(xs)) * REC_BYTES, dtype=torch.uint8, device=dev)
+
+        def step():
+            engine.launch(xs, wavelet, level, pct, outs=outs, carry_level=False, flatten=args.flatten,
+                          results=res_buf)
 
     for _ in range(max(1, args.warmup)):
-        _, res = step()
+        step()
     torch.cuda.synchronize()
-    recs = engine.decode(res, len(xs))
+    if sharded:
+        _, recs_all = assemble(gathered.view(world, -1), plan)
+        recs = [recs_all[i] for i in plan.mine[rank]]
+    else:
+        host = res_buf.cpu().numpy().view(engine.RESULT_DTYPE)[:len(xs)]
+        recs = [{k: r[k].item() for k in engine.RESULT_DTYPE.names} for r in host]
+    faults = sum(1 for r in recs if r["path"] == engine.MODE_FAULT)
     pop = sum(r["coeff_numel"] for r in recs)
+    resident = (not args.no_resident and not args.flatten and recs and all(r["eff_level"] == 0 for r in recs)
+                and len(xs) <= 24 and sum(-(-x.numel() // 49152) for x in xs) <= engine.resident_capacity())
+    has_dwt = any(r["eff_level"] > 0 for r in recs)
 
+    # ------------------------------------------------- hipGraph (single-process configs)
     G = max(1, min(args.graph_steps, args.steps))
     graph = None
-    if not args.no_graph:
+    if not args.no_graph and world == 1:
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -134,155 +284,250 @@ def main():
             graph.replay()
         torch.cuda.synchronize()
 
-    def timed(K, flush=None):
+    def max_over_ranks(t):
+        if world == 1:
+            return t
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    def timed(K, fn=None):
+        fn = fn or step
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if graph is not None and flush is None:
+        if graph is not None and fn is step:
             for _ in range(K // G):
                 graph.replay()
             for _ in range(K % G):
                 step()
         else:
             for _ in range(K):
-                if flush is not None:
-                    flush()
-                step()
+                fn()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        t = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([t], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            t = float(tt.item())
-        return t
+        return max_over_ranks(time.perf_counter() - t0)
 
+    # ------------------------------------------------------------ the headline
     K = args.steps
     T = timed(K)
     ms_per_step = T / K * 1e3
-    value = world * n_w * K / T
+    value = n_model * K / T
+    if args.profile_child:
+        return
 
-    # ---- per-stage device durations: HIP events the library records between its launches on
-    # the stream it runs on (wtp_set_stage_events); a spin kernel in front lets the whole call be
-    # enqueued before it runs, so the events time the device, not the host; caches stay as warm
-    # as in the timed loop (the same state rocprofv3's kernel trace of this command sees) ----
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(STAGES) + 1)]
-    for e in evs:
-        e.record()
-    torch.cuda.synchronize()
-    handles = (ctypes.c_void_p * len(evs))(*[e.cuda_event for e in evs])
-    per = {st: [] for st in STAGES}
-    N.lib().wtp_set_stage_events(handles, len(evs))
-    try:
-        for _ in range(args.stage_reps):
-            torch.cuda._sleep(1_000_000)  # ~0.5 ms spin on the same stream
-            step()
-            torch.cuda.synchronize()
-            for i, st in enumerate(STAGES):
-                per[st].append(evs[i].elapsed_time(evs[i + 1]) * 1e3)  # us
-    finally:
-        N.lib().wtp_set_stage_events(None, 0)
-    stage_us = {st: float(np.median(v)) for st, v in per.items()}
-    # level-0 groups within the co-resident grid run as ONE launch (k_resident): the library
-    # records stages 1-3 back to back in front of it, so "k_mask_select" times that launch
-    resident = (not args.no_resident and all(r["eff_level"] == 0 for r in recs) and len(xs) <= 24
-                and sum(-(-x.numel() // 49152) for x in xs) <= engine.resident_capacity())
-    kernel_of = dict(KERNEL_OF_STAGE, k_mask_select="k_resident") if resident else KERNEL_OF_STAGE
-    if resident:
-        stage_us = {("k_resident" if st == "k_mask_select" else st): v for st, v in stage_us.items()
-                    if st not in ("k_window", "k_collect")}
-    has_dwt = any(r["eff_level"] > 0 for r in recs)
+    # per-replay distribution (>= 50 replays of G steps, each bracketed by events on the stream)
+    dist_ms = None
+    if graph is not None:
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.replays)]
+        for a, b in evs:
+            a.record()
+            graph.replay()
+            b.record()
+        torch.cuda.synchronize()
+        per = np.array([a.elapsed_time(b) / G for a, b in evs])
+        dist_ms = {"replays": len(evs), "steps_per_replay": G, "p10": float(np.percentile(per, 10)),
+                   "p50": float(np.percentile(per, 50)), "p90": float(np.percentile(per, 90))}
 
-    def per_stage(st):
-        return float(np.median(per[st]))
-    dom = max((st for st in STAGES if stage_bytes(st, n_w, pop, has_dwt) > 0), key=lambda st: per_stage(st))
-    dom_bytes = stage_bytes(dom, n_w, pop, has_dwt)
-    achieved = dom_bytes / (per_stage(dom) * 1e-6) / 1e9
-    # a DWT stage is one launch per level (every level of these workloads takes the tiled path in
-    # one grouped launch); the PMC summary holds bytes per launch averaged over the levels
-    dom_launches = max(r["eff_level"] for r in recs) if dom in DWT_STAGES else 1
-    dom_traffic = pmc_traffic(args.config, kernel_of.get(dom, dom))
+    # ------------------------------------- dominant kernel: in-kernel launch span
+    def stamp_spans(reps, before=None):
+        st = torch.empty((reps, 2), dtype=torch.int64, device=dev)
+        st[:, 0] = -1  # ~0 as unsigned
+        st[:, 1] = 0
+        torch.cuda.synchronize()
+        base = st.data_ptr()
+        try:
+            for i in range(reps):
+                if before is not None:
+                    before()
+                L.wtp_set_kernel_stamps(ctypes.c_void_p(base + 16 * i))
+                step() if not sharded else compute()
+        finally:
+            L.wtp_set_kernel_stamps(None)
+        torch.cuda.synchronize()
+        h = st.cpu().numpy().view(np.uint64)
+        return (h[:, 1] - h[:, 0]).astype(np.float64) * 0.01  # 100 MHz ticks -> us
 
+    stage_us, dom, dom_us, dom_bytes, dom_launches, timing_src = {}, None, None, 0, 1, None
+    if resident and xs:
+        spans = stamp_spans(args.stamp_reps)
+        dom, dom_us, dom_bytes = "k_resident", float(np.mean(spans)), 8 * n_w
+        timing_src = ("in-kernel s_memrealtime stamps: first workgroup start -> last workgroup end after its "
+                      "stores completed, mean of %d back-to-back launches (wtp_set_kernel_stamps)" % len(spans))
+        stage_us = {"k_resident": dom_us}
+    elif xs:
+        # stage intervals from HIP events the library records between its launches (include dispatch
+        # gaps); a spin kernel in front lets the whole call be enqueued before it runs
+        sevs = [torch.cuda.Event(enable_timing=True) for _ in range(len(STAGES) + 1)]
+        for e in sevs:
+            e.record()
+        torch.cuda.synchronize()
+        handles = (ctypes.c_void_p * len(sevs))(*[e.cuda_event for e in sevs])
+        per_st = {st: [] for st in STAGES}
+        L.wtp_set_stage_events(handles, len(sevs))
+        try:
+            for _ in range(args.stage_reps):
+                torch.cuda._sleep(1_000_000)
+                step() if not sharded else compute()
+                torch.cuda.synchronize()
+                for i, st in enumerate(STAGES):
+                    per_st[st].append(sevs[i].elapsed_time(sevs[i + 1]) * 1e3)
+        finally:
+            L.wtp_set_stage_events(None, 0)
+
+        def sbytes(st):
+            if st in DWT_STAGES and not has_dwt:
+                return 0
+            return {"forward_dwt": 4 * n_w + 4 * pop, "k_window": 0, "k_collect": 4 * pop,
+                    "k_mask_select": 8 * n_w if pop == n_w else 0, "inverse_dwt": 4 * pop + 4 * n_w}[st]
+        ran = [st for st in STAGES if not (st in DWT_STAGES and not has_dwt)]
+        stage_us = {st: float(np.median(per_st[st])) for st in ran}
+        dom = max((st for st in ran if sbytes(st) > 0), key=lambda st: stage_us[st])
+        dom_us, dom_bytes = stage_us[dom], sbytes(dom)
+        dom_launches = max(r["eff_level"] for r in recs) if dom in DWT_STAGES else 1
+        timing_src = ("HIP events around the stage on the library's stream (median of %d calls; the interval "
+                      "includes dispatch gaps)" % args.stage_reps)
+    dom_kernel = dom if dom == "k_resident" else KERNEL_OF_STAGE.get(dom, dom)
+    if dom_us is not None and dom_us > ms_per_step * 1e3 and world == 1:
+        timing_src += "; capped at ms_per_step"
+        dom_us = ms_per_step * 1e3
+    traffic, traffic_src, traffic_tag = pmc_traffic(args.config, dom_kernel) if dom else (None, None, None)
+    stamps_us = dom_us if dom == "k_resident" else None
+    prof_us, prof_calls = rocprof_avg_us(prof_stats, dom_kernel) if dom else (None, 0)
+    if prof_us is not None:
+        # the launch duration rocprofv3 records for the dominant kernel in the child run of this
+        # configuration (dispatch to completion, what profiles/ summaries hold); per stage:
+        # launches_per_stage x the average
+        dom_us = prof_us * dom_launches
+        timing_src = ("rocprofv3 --kernel-trace --stats of this configuration's step loop, run as a child of "
+                      "this bench (%d launches of %s, average)" % (prof_calls, dom_kernel))
+
+    # ------------------------------------------------ cold Infinity Cache (MALL)
     cold = None
-    if args.cold:
-        flush_buf = torch.empty(512 << 20 >> 2, dtype=torch.float32, device=dev)
-        Kc = max(10, K // 10)
-        # time flush alone, subtract it (the flush is not part of the path)
+    if not args.no_cold and not sharded and xs:
+        flush = torch.empty(512 << 20 >> 2, dtype=torch.float32, device=dev)
+        cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.cold_reps)]
+        for a, b in cev:
+            flush.fill_(1.0)
+            a.record()
+            step()
+            b.record()
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(Kc):
-            flush_buf.fill_(1.0)
-        torch.cuda.synchronize()
-        tf = time.perf_counter() - t0
-        tc = timed(Kc, flush=lambda: flush_buf.fill_(1.0))
-        cold = {"ms_per_step": (tc - tf) / Kc * 1e3, "note": "Infinity Cache flushed by a 512 MiB write per step"}
+        cms = np.array([a.elapsed_time(b) for a, b in cev])
+        cold = {"ms_per_step_p50": float(np.median(cms)), "ms_per_step_p10": float(np.percentile(cms, 10)),
+                "ms_per_step_p90": float(np.percentile(cms, 90)), "reps": len(cev),
+                "note": "a 512 MiB write between steps evicts the 256 MiB Infinity Cache; eager launches, "
+                        "per-step HIP events (include the launch's dispatch gap)"}
+        if resident:
+            cspans = stamp_spans(args.cold_reps, before=lambda: flush.fill_(1.0))
+            cus = float(np.mean(cspans))
+            cold["k_resident_us"] = cus
+            cold["roofline_frac"] = dom_bytes / (cus * 1e-6) / 1e9 / HBM_PEAK_GBS
+        del flush
 
-    # ---- cfg4: one model LPT-sharded over the ranks + one RCCL all-gather ----
-    sharded = None
-    if world > 1 and args.config == "cfg2":
-        from wavelettransforms_amd.sharding import prune_sharded
-        base = [engine.synth(s, seed, tid, e, device=dev) for (_, s, seed, tid, e) in workload("cfg2", 0, 0)[4]]
+    # ------------------------------------------------- N > 1 legs (cfg4 split, replicas)
+    multi = None
+    if sharded:
+        Kc = max(20, K // 4)
+        t_comp = timed(Kc, compute) / Kc * 1e3
+        t_gath = timed(Kc, gather) / Kc * 1e3
+        rep_outs = [torch.empty_like(x) for x in xs_all]
+        rep_res = torch.empty(len(xs_all) * REC_BYTES, dtype=torch.uint8, device=dev)
 
-        def fn(sub):
-            return engine.prune(sub, wavelet, level, pct, carry_level=False)
-
+        def replica():
+            engine.launch(xs_all, wavelet, level, pct, outs=rep_outs, carry_level=False, results=rep_res)
         for _ in range(3):
-            prune_sharded(base, wavelet, level, pct, fn)
-        dist.barrier()
-        torch.cuda.synchronize()
-        Ks = 20
-        t0 = time.perf_counter()
-        for _ in range(Ks):
-            _, _, plan = prune_sharded(base, wavelet, level, pct, fn)
-        torch.cuda.synchronize()
-        dist.barrier()
-        ts_ = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        dist.all_reduce(ts_, op=dist.ReduceOp.MAX)
-        sharded = {"ms_per_step": float(ts_.item()) / Ks * 1e3, "max_rank_weights": int(plan.max_shard),
-                   "note": "one model, LPT layer shards + all_gather_into_tensor (RCCL), host-synchronous"}
+            replica()
+        t_rep = timed(Kc, replica) / Kc * 1e3
+        multi = {"cfg4_one_model": {"end_to_end_ms": ms_per_step, "compute_ms_max_rank": t_comp,
+                                    "all_gather_ms": t_gath, "max_rank_weights": int(plan.max_shard),
+                                    "gathered_bytes_per_rank": int(world * plan.slice * 4),
+                                    "note": "LPT layer shards pruned into the flat shard, one all_gather_into_tensor "
+                                            "(RCCL) of weights + records; eager launches"},
+                 "replicas": {"value": world * n_model / (t_rep * 1e-3), "ms_per_step": t_rep, "scaling": "weak",
+                              "note": "every rank prunes its own full model, no collective"}}
 
-    # ---- CPU baseline: the C oracle (port of the reference's arithmetic) on host cores ----
+    # --------------------------------------------- CPU baseline (rank 0, N = 1 only)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         from oracle import oracle as O
-        host = [O.synth(s, seed, tid, e) for (_, s, seed, tid, e) in ts]
-        O.prune_batch(host[:1], wavelet, level, pct)
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            O.prune_batch(host, wavelet, level, pct, nthreads=1)
-            reps += 1
-            if time.perf_counter() - t0 >= args.cpu_seconds:
-                break
-        tcpu = time.perf_counter() - t0
-        cpu = {"value": n_w * reps / tcpu, "unit": "weight-coeffs/s", "cores": 1, "kind": "port",
-               "sample": "%d full passes over the %s workload (%d weights) with the single-threaded C "
-                         "restatement (oracle/wtprune_oracle.c), %.1f s" % (reps, name, n_w, tcpu)}
+        host = [O.synth(s, seed, tid, e) for (s, seed, tid, e) in mine]
+        if args.config == "cfg5":
+            host = host[:2]  # bounded sample: two 4096^2 blocks
+        n_host = sum(h.size for h in host)
+
+        def leg(nthreads, seconds):
+            O.prune_batch(host[:1], wavelet, level, pct, nthreads=nthreads)
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                O.prune_batch(host, wavelet, level, pct, nthreads=nthreads)
+                reps += 1
+                if time.perf_counter() - t0 >= seconds:
+                    break
+            return reps, time.perf_counter() - t0
+        nt = min(cpu_threads(), O.max_threads())
+        r1, t1 = leg(1, args.cpu_seconds / 2)
+        rn, tn = leg(nt, args.cpu_seconds / 2)
+        try:
+            import pywt  # noqa: F401
+            pywt_note = "importable (not timed: third-party, not the reference)"
+        except Exception as exc:
+            pywt_note = "unavailable on this host (%s): the reference's PyWavelets path cannot run here" % type(exc).__name__
+        cpu = {"value": n_host * rn / tn, "unit": "weight-coeffs/s", "cores": nt, "kind": "port",
+               "cpu_model": cpu_model(), "pywt": pywt_note,
+               "sample": "%d passes over %d weights of the %s workload with the C restatement "
+                         "(oracle/wtprune_oracle.c, OpenMP over tensors, %d threads), %.1f s"
+                         % (rn, n_host, name, nt, tn),
+               "single_thread": {"value": n_host * r1 / t1, "cores": 1,
+                                 "sample": "%d passes, %.1f s (the reference's execution model: one thread)"
+                                           % (r1, t1)}}
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "weight-coeffs/s", "n_gpus": world, "steps": K,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "strong" if world > 1 else "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (splitmix64 Irwin-Hall, kaiming-scaled)",
-            "config": {"workload": name, "config": args.config, "wavelet": wavelet, "level": level,
-                       "percentile": pct, "weights_per_gpu_step": n_w, "coeffs_per_gpu_step": pop,
-                       "tensors": len(xs), "eff_levels": sorted({r["eff_level"] for r in recs}),
-                       "graph_steps": G if graph is not None else 0, "parallelism": "replica%d" % world,
+            "config": {"workload": name, "config": args.config if not sharded else "cfg4",
+                       "wavelet": wavelet, "level": level, "percentile": pct, "weights_per_step": n_model,
+                       "weights_this_rank": n_w, "coeffs_this_rank": pop, "tensors": len(model),
+                       "eff_levels": sorted({r["eff_level"] for r in recs}),
+                       "graph_steps": G if graph is not None else 0,
+                       "parallelism": ("lpt-layer-shard%d+allgather" % world if sharded
+                                       else ("block-split%d" % world if world > 1 else "single")),
                        "transform": "1-D flattened (extension)" if args.flatten else "2-D over (kh, kw) (reference)"},
-            "pipeline_hbm_gbs": 8 * n_w * K / T / 1e9,
-            "roofline": {"bound": "hbm", "kernel": kernel_of.get(dom, dom), "stage": dom,
-                         "launches_per_stage": dom_launches, "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": (None if dom_traffic is None else dom_traffic * dom_launches),
-                         "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_us": per_stage(dom)},
+            "pipeline_hbm_gbs": 8 * n_model * K / T / 1e9,
+            "step_distribution_ms": dist_ms,
+            "roofline": None if dom is None else {
+                "bound": "hbm", "kernel": dom_kernel, "stage": dom, "launches_per_stage": dom_launches,
+                "achieved": dom_bytes / (dom_us * 1e-6) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": dom_bytes / (dom_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                "traffic": None if traffic is None else traffic * dom_launches,
+                "traffic_source": traffic_src and ("committed rocprofv3 --pmc summary %s (2 x FETCH_SIZE + "
+                                                   "WRITE_SIZE per launch), not measured in this run" % traffic_src),
+                "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_us": dom_us, "timing": timing_src,
+                "avg_launch_us_stamps": stamps_us, "pmc_source_tag": traffic_tag},
             "stage_us": stage_us,
             "cpu_baseline": cpu,
         }
+        if faults:
+            line["resident_faults"] = faults
+        if args.config == "cfg5":
+            flops = DB8_L5_FLOP_PER_ELEM * n_model
+            line["valu_roof"] = {"flop_per_elem": DB8_L5_FLOP_PER_ELEM, "peak_tflops": VALU_NOFMA_TFLOPS,
+                                 "floor_ms": flops / (VALU_NOFMA_TFLOPS * 1e12) * 1e3 / world,
+                                 "frac": flops / (T / K) / (VALU_NOFMA_TFLOPS * 1e12) / world,
+                                 "note": "pipeline vs the no-FMA FP32 VALU roof (bit-exactness forbids contraction)"}
         if cold:
             line["cold_mall"] = cold
-        if sharded:
-            line["cfg4_sharded_one_model"] = sharded
+        if multi:
+            line.update(multi)
+        if rehearsal and world > 1:
+            line["rehearsal"] = "all ranks on one GPU over gloo: a functional check, not a measurement"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

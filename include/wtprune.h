@@ -106,9 +106,12 @@ int wtp_prune_layers_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id
  * over the list under WTP_CARRY_LEVEL), packed by pywt.coeffs_to_array ([cA_L | cD_L | ... |
  * cD_1]), thresholded at the pct-th percentile of |coeffs| exactly as the 2-D path, rebuilt by
  * pywt.waverec and cut to numel; ndim < 2 tensors keep the plain-percentile branch (:58-62).
+ * WTP_NO_RESIDENT forces the three-launch form of level-0 groups for this call only (the retry of
+ * tensors whose resident launch recorded WTP_PATH_FAULT).
  * Workspace: wtp_workspace_size_ex with the same flags. */
 #define WTP_CARRY_LEVEL 1
 #define WTP_FLATTEN 2
+#define WTP_NO_RESIDENT 4
 size_t wtp_workspace_size_ex(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, int flags);
 int wtp_prune_ex_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, int flags,
                      void* workspace, size_t workspace_bytes, wtp_result* results_dev, wtp_stream_t stream);
@@ -175,6 +178,11 @@ int wtp_resident_capacity(void); /* 0 if the current device cannot host the resi
  * Default 200000; tests lower it to force the fault path. */
 unsigned wtp_set_resident_timeout_us(unsigned us);
 #define WTP_PATH_FAULT 99
+/* measurement hook (bench.py): while set, every resident launch atomically lowers stamps_dev[0] to
+ * its first workgroup's start and raises stamps_dev[1] to its last workgroup's end (after that
+ * workgroup's stores completed), in ticks of the 100 MHz wall clock -- the launch's span on the
+ * device, free of the host's dispatch gaps.  The caller initialises [0] = ~0, [1] = 0; NULL = off. */
+int wtp_set_kernel_stamps(unsigned long long* stamps_dev);
 
 const char* wtp_last_error(void);
 int wtp_last_error_tensor(void); /* index of the tensor that failed validation, or -1 */

@@ -200,11 +200,19 @@ def test_in_place_and_workspace_reuse(eng):
 
 
 def test_perfect_reconstruction_full_size(eng):
-    """Size-independent property at the cfg5 block size: waverec2(wavedec2(x)) == oracle, and
-    within PyWavelets' float32 perfect-reconstruction tolerance of x."""
-    x = eng.synth((4096, 4096), 5, 7, G.W.sigma_exponent((2.0 / 4096) ** 0.5))
+    """At the cfg5 block size: waverec2(wavedec2(x)) equals the oracle's round trip bit for bit
+    (the oracle at percentile 0 prunes nothing, so its output IS waverec2(wavedec2(x))), the packed
+    coefficients equal the oracle's, and the round trip is within PyWavelets' float32
+    perfect-reconstruction tolerance of x (RMS < 6e-7 * max|x|, pywt/tests/test_perfect_reconstruction.py)."""
+    e = G.W.sigma_exponent((2.0 / 4096) ** 0.5)
+    x = eng.synth((4096, 4096), 5, 7, e)
     P = eng.wavedec2_packed(x, "db8", 5)
     y = eng.waverec2_packed(P, (4096, 4096), "db8", 5)
+    host = G.W.synth_numpy((4096, 4096), 5, 7, e)
+    ref, rr, coeffs = O.prune_tensor(host, "db8", 5, 0.0, want_coeffs=True)
+    assert rr["zero_count"] == int((ref == 0).sum())
+    assert np.array_equal(P.cpu().numpy().view(np.uint32), coeffs.view(np.uint32))
+    assert np.array_equal(y.cpu().numpy(), ref)
     err = (y - x).float()
     rms = float(torch.sqrt(torch.mean(err * err)))
     assert rms < 6e-7 * float(x.abs().max())

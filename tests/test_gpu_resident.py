@@ -171,3 +171,77 @@ def test_alternating_forms_share_the_workspace(eng):
         for a, b, ra, rb in zip(first, outs, r0, res):
             assert torch.equal(a, b) and ra["zero_count"] == rb["zero_count"]
     eng.set_resident(True)
+
+
+@pytest.fixture
+def short_waits(eng):
+    """Every wait of the resident launch bounded by 0 us: workgroups that find their segment's
+    barrier incomplete on the first poll time out (wtp_set_resident_timeout_us)."""
+    from wavelettransforms_amd import _native as N
+    prev = N.lib().wtp_set_resident_timeout_us(0)
+    yield
+    N.lib().wtp_set_resident_timeout_us(prev)
+
+
+def test_timeout_stores_nothing_in_place(eng, short_waits):
+    """A resident launch whose waits time out must leave the caller's tensors untouched (in place:
+    the input IS the output) and flag the tensors MODE_FAULT; the others are exact."""
+    ts = G.W.resnet18_tensors(0)
+    host = [G.W.synth_numpy(s, seed, tid, e) for _, s, seed, tid, e in ts]
+    xs = [_dev(x) for x in host]
+    _, res = eng.launch(xs, "bior3.3", 5, 50.0, outs=xs, carry_level=False)
+    torch.cuda.synchronize()
+    bad = eng.fault_mask(res, len(xs))
+    assert bad.any(), "a 0 us bound should fault the multi-workgroup segments"
+    for i, (x, h) in enumerate(zip(xs, host)):
+        if bad[i]:
+            assert np.array_equal(x.cpu().numpy().view(np.uint32), h.view(np.uint32)), "faulted tensor %d modified" % i
+        else:
+            ref, _ = O.prune_tensor(h, "bior3.3", 5, 50.0)
+            assert np.array_equal(x.cpu().numpy(), ref)
+
+
+def test_timeout_retried_by_prune(eng, short_waits):
+    """engine.prune re-runs the faulted tensors in the three-launch form: the results equal the
+    oracle, in place and out of place, per layer and with the level carried over the list."""
+    ts = G.W.resnet18_tensors(0)
+    host = [G.W.synth_numpy(s, seed, tid, e) for _, s, seed, tid, e in ts]
+    for inplace in (True, False):
+        for carry in (False, True):
+            xs = [_dev(x) for x in host]
+            outs, recs = eng.prune(xs, "bior3.3", 5, 50.0, outs=xs if inplace else None, carry_level=carry)
+            for h, o, r in zip(host, outs, recs):
+                ref, rr = O.prune_tensor(h, "bior3.3", 5, 50.0)
+                _same(o.cpu().numpy(), ref, r, rr)
+                assert r["path"] != eng.MODE_FAULT
+
+
+def test_workspace_per_stream(eng):
+    """Calls on two streams at once use distinct workspaces (the selection state lives there)."""
+    ts = G.W.resnet18_tensors(0)[:8]
+    host = [G.W.synth_numpy(s, seed, tid, e) for _, s, seed, tid, e in ts]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    xa = [_dev(x) for x in host]
+    xb = [_dev(-x) for x in host]
+    torch.cuda.synchronize()
+    got = {}
+    for name, s, xs in (("a", s1, xa), ("b", s2, xb)):
+        with torch.cuda.stream(s):
+            got[name] = eng.launch(xs, "bior3.3", 5, 37.5, carry_level=False, stream=s)
+    torch.cuda.synchronize()
+    assert eng.workspace(xa[0].device, 256, s1).data_ptr() != eng.workspace(xa[0].device, 256, s2).data_ptr()
+    for name, sign in (("a", 1.0), ("b", -1.0)):
+        outs, res = got[name]
+        for h, o, r in zip(host, outs, eng.decode(res, len(outs))):
+            ref, rr = O.prune_tensor(sign * h, "bior3.3", 5, 37.5)
+            _same(o.cpu().numpy(), ref, r, rr)
+
+
+def test_outs_validated(eng):
+    x = eng.synth((64, 64, 3, 3), 1, 1, 26)
+    with pytest.raises(ValueError):
+        eng.launch([x], "bior3.3", 5, 50.0, outs=[torch.empty(64, 64, 3, 6, device="cuda")[..., ::2]])
+    with pytest.raises(ValueError):
+        eng.launch([x], "bior3.3", 5, 50.0, outs=[torch.empty(10, device="cuda")])
+    with pytest.raises(TypeError):
+        eng.launch([x], "bior3.3", 5, 50.0, outs=[torch.empty(64, 64, 3, 3, device="cuda", dtype=torch.float64)])

@@ -1,6 +1,7 @@
 """cfg4 sharding: LPT plan and the all-gather reassembly, world_size 2 over gloo on
-the CPU.  The per-rank prune function is a test double (the C oracle, layer by layer); on the GPU
-the same code path runs engine.prune over RCCL."""
+the CPU.  The per-rank prune function is a test double (the C oracle, layer by layer, writing into
+the flat-shard views); on the GPU the same code path runs engine.launch over RCCL
+(tests/test_gpu_sharding.py)."""
 import os
 import socket
 
@@ -33,16 +34,16 @@ def test_lpt_plan_resnet18():
 def _oracle_prune(wavelet, level, pct):
     from oracle import oracle as O
 
-    def fn(sub):
-        outs, recs = [], []
-        for x in sub:
+    def fn(sub, outs):
+        recs = []
+        for x, y in zip(sub, outs):
             o, r = O.prune_tensor(x.numpy(), wavelet, level, pct)
-            outs.append(torch.from_numpy(np.ascontiguousarray(o)))
+            y.copy_(torch.from_numpy(np.ascontiguousarray(o)))
             recs.append({"numel": r["numel"], "zero_count": r["zero_count"], "coeff_numel": r["coeff_numel"],
                          "thr64": r["thr64"], "eff_level": r["eff_level"], "path": 0,
                          "thr32_bits": int(np.float32(r["thr32"]).view(np.uint32)),
                          "max_abs_bits": int(np.float32(r["max_abs"]).view(np.uint32))})
-        return outs, recs
+        return recs
     return fn
 
 

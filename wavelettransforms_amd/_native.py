@@ -82,6 +82,7 @@ def lib():
             "wtp_set_resident": ([i32], i32),
             "wtp_resident_capacity": ([], i32),
             "wtp_set_resident_timeout_us": ([ctypes.c_uint], ctypes.c_uint),
+            "wtp_set_kernel_stamps": ([vp], i32),
             "wtp_last_error": ([], ctypes.c_char_p),
             "wtp_last_error_tensor": ([], i32),
         }

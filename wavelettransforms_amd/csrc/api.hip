@@ -425,6 +425,10 @@ int wtp_set_resident(int mode) {
 }
 int wtp_resident_capacity(void) { return resident_capacity(); }
 unsigned wtp_set_resident_timeout_us(unsigned us) { return set_resident_timeout_us(us); }
+int wtp_set_kernel_stamps(unsigned long long* stamps_dev) {
+    set_kernel_stamps(stamps_dev);
+    return WTP_OK;
+}
 
 size_t wtp_workspace_size(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level) {
     if (ntensors < 0 || (ntensors > 0 && !tensors)) return 0;
@@ -443,7 +447,8 @@ int wtp_workspace_init(void* ws, size_t bytes, wtp_stream_t stream) {
 }
 
 static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, void* ws,
-                      size_t ws_bytes, wtp_result* results, wtp_stream_t stream, bool carry, bool flat = false) {
+                      size_t ws_bytes, wtp_result* results, wtp_stream_t stream, bool carry, bool flat = false,
+                      bool no_resident = false) {
     g_err.clear();
     g_err_tensor = -1;
     if (ntensors < 0 || (ntensors > 0 && (!tensors || !results))) return fail(WTP_EARG, -1, "bad arguments");
@@ -497,7 +502,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             all0 = all0 && !ps[t].dwt;
             rblk += (ps[t].pop + RES_CHUNK - 1) / RES_CHUNK;
         }
-        const bool resident = all0 && g_resident.load(std::memory_order_relaxed) && rblk <= RES_MAX_WG &&
+        const bool resident = all0 && !no_resident && g_resident.load(std::memory_order_relaxed) && rblk <= RES_MAX_WG &&
                               rblk <= resident_capacity();
         const int64_t chunk = resident ? RES_CHUNK : CHUNK;
         SegTable tab;
@@ -569,7 +574,7 @@ int wtp_prune_layers_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id
 }
 
 size_t wtp_workspace_size_ex(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, int flags) {
-    if (ntensors < 0 || (ntensors > 0 && !tensors) || (flags & ~(WTP_CARRY_LEVEL | WTP_FLATTEN))) return 0;
+    if (ntensors < 0 || (ntensors > 0 && !tensors) || (flags & ~(WTP_CARRY_LEVEL | WTP_FLATTEN | WTP_NO_RESIDENT))) return 0;
     std::vector<TPlan> ps;
     if (plan_tensors(tensors, ntensors, wavelet_id, level, 50.0, false, ps, (flags & WTP_CARRY_LEVEL) != 0,
                      (flags & WTP_FLATTEN) != 0) != WTP_OK)
@@ -579,9 +584,9 @@ size_t wtp_workspace_size_ex(const wtp_tensor* tensors, int ntensors, int wavele
 
 int wtp_prune_ex_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, int flags,
                      void* ws, size_t ws_bytes, wtp_result* results, wtp_stream_t stream) {
-    if (flags & ~(WTP_CARRY_LEVEL | WTP_FLATTEN)) return fail(WTP_EARG, -1, "bad flags 0x%x", flags);
+    if (flags & ~(WTP_CARRY_LEVEL | WTP_FLATTEN | WTP_NO_RESIDENT)) return fail(WTP_EARG, -1, "bad flags 0x%x", flags);
     return prune_impl(tensors, ntensors, wavelet_id, level, pct, ws, ws_bytes, results, stream,
-                      (flags & WTP_CARRY_LEVEL) != 0, (flags & WTP_FLATTEN) != 0);
+                      (flags & WTP_CARRY_LEVEL) != 0, (flags & WTP_FLATTEN) != 0, (flags & WTP_NO_RESIDENT) != 0);
 }
 
 /* ---------------------------------------------------------- min pruning --- */

@@ -1566,6 +1566,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader*
     __shared__ uint32_t wred[RES_THREADS / 64][8];
     __shared__ uint32_t wstage[(RES_STG + 1) * RES_THREADS]; /* 66 KB: RES_STG slots + the discard slot per thread */
     const uint32_t q = head->parity;
+    if (t.stamps && threadIdx.x == 0) atomicMin(t.stamps, wall_ticks()); /* measurement only */
     {   /* clear this workgroup's slice of the idle region (the previous launch's) */
         uint4* idle = reinterpret_cast<uint4*>(sel_region(head, q ^ 1u));
         constexpr int NV4 = (int)(SEL_REGION / 16);
@@ -1583,6 +1584,11 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader*
         res_body<true>(t, sd, head, q, cand, res, thr_out, base, len, raw, lsub, wred, wstage);
     else
         res_body<false>(t, sd, head, q, cand, res, thr_out, base, len, raw, lsub, wred, wstage);
+    if (t.stamps) { /* measurement only: the workgroup's end, once its stores have completed */
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(t.stamps + 1, wall_ticks());
+    }
 }
 
 /* The in-place segments whose k_mask_select took the full-scan select: the mask pass that
@@ -2025,12 +2031,15 @@ int resident_capacity() {
 }
 static std::atomic<uint32_t> g_res_timeout_us{RES_TIMEOUT_DEFAULT_US};
 uint32_t set_resident_timeout_us(uint32_t us) { return g_res_timeout_us.exchange(us); }
+static std::atomic<unsigned long long*> g_stamps{nullptr};
+void set_kernel_stamps(unsigned long long* dev) { g_stamps.store(dev); }
 void launch_resident(const SegTable& t0, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
                      hipStream_t s) {
     static const int sig = [] { const char* e = getenv("WTP_RES_SIGMA"); return e && atoi(e) > 0 ? atoi(e) : RES_SIGMA_X100; }();
     SegTable t = t0;
     t.pad[1] = sig; /* window margin: sig/100 binomial sigma + 8 sample ranks */
     t.res_timeout = g_res_timeout_us.load(std::memory_order_relaxed) * 100u; /* 100 MHz wall clock */
+    t.stamps = g_stamps.load(std::memory_order_relaxed);
     hipLaunchKernelGGL(k_resident, dim3(t.nblk), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
 }
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,

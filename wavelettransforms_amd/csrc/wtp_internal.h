@@ -95,6 +95,7 @@ struct SegTable {
     int32_t pad[2];
     uint32_t res_timeout; /* k_resident: bound of every wait, in ticks of the 100 MHz wall clock */
     int32_t pad2;
+    unsigned long long* stamps; /* k_resident: [0] min start, [1] max end (100 MHz ticks); null = off */
     int32_t blk_begin[SEG_PER_LAUNCH]; /* INT32_MAX past nseg: block -> segment in one scalar sweep */
     SegDesc s[SEG_PER_LAUNCH];
 };
@@ -196,7 +197,8 @@ constexpr int RES_WG_WORDS = RES_SLOT_WORDS;        /* one workgroup's slot in t
 constexpr int RES_SEL_MAX = 1024;                   /* keys the one-wave select takes (more: full scan) */
 constexpr uint32_t RES_TIMEOUT_DEFAULT_US = 200000; /* a wait this long means the grid is not co-resident */
 int resident_capacity();
-uint32_t set_resident_timeout_us(uint32_t us); /* every k_resident wait's bound; returns the previous one */                            /* co-resident workgroups on the current device */
+uint32_t set_resident_timeout_us(uint32_t us); /* every k_resident wait's bound; returns the previous one */
+void set_kernel_stamps(unsigned long long* dev); /* k_resident launch span stamps (measurement) */                            /* co-resident workgroups on the current device */
 void launch_resident(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
                      hipStream_t s);
 /* min-weight pruning after window + collect: mp = 16 B per tensor, tiecnt = one u32 per

@@ -23,15 +23,43 @@ def wavelet_id(name):
     return N.lib().wtp_wavelet_id(str(name).encode()) if isinstance(name, str) else -1
 
 
-def workspace(device, nbytes):
-    """Grow-only, zero-initialised workspace per device (the library keeps it clean between calls)."""
+def workspace(device, nbytes, stream=None):
+    """Grow-only, zero-initialised workspace per (device, stream): the selection, barrier and
+    parity state of a call live in it, so calls on distinct streams need distinct workspaces
+    (include/wtprune.h).  The library keeps it clean between calls on its stream."""
     device = torch.device(device)
-    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    if device.index is None:
+        device = torch.device(device.type, torch.cuda.current_device())
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    key = (device.index, stream.cuda_stream)
     ws = _workspaces.get(key)
     if ws is None or ws.numel() < nbytes:
-        ws = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        # allocated (and zeroed) on the call's stream, so the caching allocator ties the block to it
+        with torch.cuda.stream(stream):
+            ws = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         _workspaces[key] = ws
     return ws
+
+
+def _results(n, device, stream):
+    with torch.cuda.stream(stream):
+        return torch.empty(n * N.RESULT_BYTES, dtype=torch.uint8, device=device)
+
+
+def check_outs(tensors, outs):
+    """Caller-supplied outputs must be dense float32 CUDA tensors shaped like their inputs: the
+    library writes numel contiguous floats from out.data_ptr()."""
+    if len(outs) != len(tensors):
+        raise ValueError("wavelettransforms_amd: %d outputs for %d tensors" % (len(outs), len(tensors)))
+    for i, (x, y) in enumerate(zip(tensors, outs)):
+        if not isinstance(y, torch.Tensor) or not y.is_cuda or y.dtype != torch.float32:
+            raise TypeError("wavelettransforms_amd: outs[%d] must be a float32 CUDA tensor" % i)
+        if y.device != x.device or y.numel() != x.numel():
+            raise ValueError("wavelettransforms_amd: outs[%d] has %d elements on %s, input %d on %s"
+                             % (i, y.numel(), y.device, x.numel(), x.device))
+        if not y.is_contiguous():
+            raise ValueError("wavelettransforms_amd: outs[%d] is not contiguous" % i)
 
 
 def _as_desc(tensors, outs):
@@ -89,19 +117,25 @@ def check_tensors(tensors):
             raise TypeError("wavelettransforms_amd: float32 weights only (got %s)" % x.dtype)
 
 
-WTP_CARRY_LEVEL, WTP_FLATTEN = 1, 2  # include/wtprune.h
+WTP_CARRY_LEVEL, WTP_FLATTEN, WTP_NO_RESIDENT = 1, 2, 4  # include/wtprune.h
 
 
-def launch(tensors, wavelet, level, pct, outs=None, carry_level=True, stream=None, flatten=False):
+def launch(tensors, wavelet, level, pct, outs=None, carry_level=True, stream=None, flatten=False,
+           no_resident=False, results=None):
     """Enqueue the path for `tensors` (CUDA float32) on `stream` (default: current stream).
     Returns (outs, results_dev) without synchronising; results_dev is a uint8 CUDA tensor of
     len(tensors) wtp_result records.  carry_level=True is multi_resolution_analysis over a
     list (the clamped level carries over, dwt_pruning.py:64-65); False is one call per layer
-    (prune_layer_weights / wavelet_pruning).  flatten=True: the 1-D flattened mode (WTP_FLATTEN)."""
+    (prune_layer_weights / wavelet_pruning).  flatten=True: the 1-D flattened mode (WTP_FLATTEN).
+    A record whose path reads MODE_FAULT was not computed (the resident launch's grid was not
+    co-resident; nothing was stored for that tensor): prune() re-runs such tensors itself.
+    results: optional uint8 CUDA tensor of len(tensors) records (8-byte aligned) to write into."""
     check_tensors(tensors)
     tensors = [x.contiguous() for x in tensors]
     if outs is None:
         outs = [torch.empty_like(x) for x in tensors]
+    else:
+        check_outs(tensors, outs)
     n = len(tensors)
     if n == 0:
         return outs, None
@@ -109,12 +143,19 @@ def launch(tensors, wavelet, level, pct, outs=None, carry_level=True, stream=Non
     L = N.lib()
     wid = wavelet_id(wavelet)
     desc = _as_desc(tensors, outs)
-    flags = (WTP_CARRY_LEVEL if carry_level else 0) | (WTP_FLATTEN if flatten else 0)
+    flags = ((WTP_CARRY_LEVEL if carry_level else 0) | (WTP_FLATTEN if flatten else 0)
+             | (WTP_NO_RESIDENT if no_resident else 0))
     nbytes = L.wtp_workspace_size_ex(desc, n, wid, int(level), flags)
-    ws = workspace(device, nbytes if nbytes else 256)
-    res = torch.empty(n * N.RESULT_BYTES, dtype=torch.uint8, device=device)
     if stream is None:
         stream = torch.cuda.current_stream(device)
+    ws = workspace(device, nbytes if nbytes else 256, stream)
+    if results is None:
+        res = _results(n, device, stream)
+    else:
+        if (results.dtype != torch.uint8 or not results.is_cuda or results.numel() < n * N.RESULT_BYTES
+                or results.data_ptr() % 8):
+            raise ValueError("wavelettransforms_amd: results must be %d 8-byte aligned CUDA bytes" % (n * N.RESULT_BYTES))
+        res = results
     rc = L.wtp_prune_ex_f32(desc, n, wid, int(level), float(pct), flags, ws.data_ptr(), ws.numel(), res.data_ptr(),
                             ctypes.c_void_p(stream.cuda_stream))
     if rc != N.WTP_OK:
@@ -122,15 +163,35 @@ def launch(tensors, wavelet, level, pct, outs=None, carry_level=True, stream=Non
     return outs, res
 
 
-MODE_FAULT = 99  # k_resident's grid was not co-resident: its barrier timed out (include/wtprune.h)
+MODE_FAULT = 99  # WTP_PATH_FAULT: the resident launch timed out for this tensor and stored nothing
+
+
+def carried_level(tensors, wavelet, level, flatten=False):
+    """The level multi_resolution_analysis passes on after `tensors` (dwt_pruning.py:64-65: every
+    tensor with ndim >= 2 clamps it to pywt.dwt_max_level of min(kh, kw) -- of numel in the
+    flattened mode)."""
+    L = N.lib()
+    F = L.wtp_dec_len(wavelet_id(wavelet))
+    lvl = int(level)
+    for x in tensors:
+        if x.dim() >= 2:
+            n = x.numel() if flatten else min(x.shape[-2], x.shape[-1])
+            lvl = min(lvl, int(L.wtp_max_level(int(n), int(F))))
+    return lvl
+
+
+def fault_mask(results_dev, n):
+    """Per-tensor flags: True where the record reads MODE_FAULT (host copy of the records)."""
+    host = results_dev.cpu().numpy().view(RESULT_DTYPE)[:n]
+    return host["path"] == MODE_FAULT
 
 
 def decode(results_dev, n):
     host = results_dev.cpu().numpy().view(RESULT_DTYPE)[:n]
     out = []
     if (host["path"] == MODE_FAULT).any():
-        raise RuntimeError("wavelettransforms_amd: the resident launch could not hold its whole grid on the GPU "
-                           "(other kernels occupied CUs); results are invalid -- call set_resident(False)")
+        raise RuntimeError("wavelettransforms_amd: records of a resident launch that timed out (MODE_FAULT); "
+                           "re-run those tensors with no_resident=True (prune() does this itself)")
     for r in host:
         d = {k: r[k].item() for k in RESULT_DTYPE.names}
         d["thr32"] = float(np.array(d["thr32_bits"], np.uint32).view(np.float32))
@@ -151,11 +212,29 @@ def resident_capacity():
 
 
 def prune(tensors, wavelet, level, pct, outs=None, carry_level=True, flatten=False):
-    """launch() + wait + decoded per-tensor records (numel, zero_count, nonzero, thr64, ...)."""
+    """launch() + wait + decoded per-tensor records (numel, zero_count, nonzero, thr64, ...).
+    Tensors whose resident launch faulted (their inputs and outputs untouched) are re-run once in
+    the three-launch form -- only those: a tensor pruned in place must not be pruned twice.  Under
+    carry_level each one re-runs at the level the list carried into it (computed from the shapes
+    of the tensors before it), as an independent call, grouped by that level."""
     outs, res = launch(tensors, wavelet, level, pct, outs=outs, carry_level=carry_level, flatten=flatten)
     if res is None:
         return outs, []
-    return outs, decode(res, len(tensors))
+    n = len(tensors)
+    bad = fault_mask(res, n)
+    if bad.any():
+        idx = [i for i in range(n) if bad[i]]
+        groups = {}
+        for i in idx:
+            lvl = carried_level(tensors[:i], wavelet, level, flatten) if carry_level else int(level)
+            groups.setdefault(lvl, []).append(i)
+        merged = res.clone().view(n, N.RESULT_BYTES)
+        for lvl, g in groups.items():
+            _, res2 = launch([tensors[i] for i in g], wavelet, lvl, pct, outs=[outs[i] for i in g],
+                             carry_level=False, flatten=flatten, no_resident=True)
+            merged[g] = res2.view(len(g), N.RESULT_BYTES)
+        res = merged.view(-1)
+    return outs, decode(res, n)
 
 
 def min_prune(tensors, fraction, outs=None):
@@ -166,6 +245,8 @@ def min_prune(tensors, fraction, outs=None):
     tensors = [x.contiguous() for x in tensors]
     if outs is None:
         outs = [torch.empty_like(x) for x in tensors]
+    else:
+        check_outs(tensors, outs)
     n = len(tensors)
     if n == 0:
         return outs, []
@@ -195,6 +276,8 @@ def random_prune(tensors, prune_counts, seed, outs=None):
     tensors = [x.contiguous() for x in tensors]
     if outs is None:
         outs = [torch.empty_like(x) for x in tensors]
+    else:
+        check_outs(tensors, outs)
     n = len(tensors)
     if n == 0:
         return outs, []
@@ -228,7 +311,10 @@ def threshold(x, pct, out=None):
     """percentile_based_thresholding (dwt_pruning.py:25-32) of a CUDA float32 tensor."""
     check_tensors([x])
     x = x.contiguous()
-    out = torch.empty_like(x) if out is None else out
+    if out is None:
+        out = torch.empty_like(x)
+    else:
+        check_outs([x], [out])
     L = N.lib()
     desc = _as_desc([x.reshape(-1)], [out.reshape(-1)])
     ws = workspace(x.device, L.wtp_workspace_size(desc, 1, -1, 0) or 256)
