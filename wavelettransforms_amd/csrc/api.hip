@@ -527,7 +527,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             sd.cand_off = (int64_t)p.cand_off;
             sd.cap = p.cap;
             bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap, p.dwt);
-            if (resident) sd.nsub_log2 = 10; /* NSUB_MAX */
+            if (resident) sd.nsub_log2 = RES_NSUB_LOG2;
             blk += (int)((p.pop + chunk - 1) / chunk);
         }
         tab.nblk = blk;

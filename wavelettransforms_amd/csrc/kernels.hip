@@ -194,6 +194,18 @@ __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, i
 #ifndef WTP_WPROBE
 #define WTP_WPROBE(i)
 #endif
+#ifndef WTP_RES_CNT /* k_resident's below / == kl counts: 1 ballot popcounts (scalar unit), 0 per-lane */
+#define WTP_RES_CNT 0
+#endif
+#ifndef WTP_RES_NTST /* k_resident's output stores: 1 nontemporal (tools/mb/reslab.hip A/B) */
+#define WTP_RES_NTST 1
+#endif
+#ifndef WTP_RES_FSEL /* k_resident's final select: 1 one-wave radix selects, 0 the block radix select */
+#define WTP_RES_FSEL 0
+#endif
+#ifndef WTP_RES_P0 /* k_resident's load order (tools/mb/reslab.hip A/B) */
+#define WTP_RES_P0 1
+#endif
 #ifndef WTP_RES_ABL /* tools/mb/reslab.hip ablations: bit 0 window, 1 count, 2 bucket scatter, 3 select, 4 barrier */
 #define WTP_RES_ABL 0
 #endif
@@ -1128,7 +1140,50 @@ __device__ __forceinline__ void window_search_flat(const SegDesc& sd, const uint
     *sh_out = sh;
 }
 
-constexpr uint32_t RES_POISON = 0x80000000u; /* a segment barrier counter whose wait timed out */
+constexpr uint32_t RES_POISON = 0x80000000u;
+
+/* Rank r (0-based, ascending) among the m keys stage[0..m), all in [lo, hi]: ONE wave, an MSB-first
+ * radix select in 8-bit digits below the common prefix of lo and hi over a private 256-bin LDS
+ * histogram h.  A wave's LDS instructions complete in order, so no barrier separates the clear,
+ * the adds and the reads -- but the compiler must not forward a lane's own clear to its read of
+ * bins other lanes added to (the asm memory clobbers).  Every lane of the wave must be active. */
+__device__ __forceinline__ uint32_t wave_radix_select(const uint32_t* stage, int m, int r, uint32_t lo, uint32_t hi,
+                                                      uint32_t* h) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t diff = lo ^ hi;
+    int top = diff ? 31 - __clz(diff) : -1; /* highest unknown bit */
+    uint32_t mask = top >= 31 ? 0u : ~((2u << top) - 1u);
+    uint32_t prefix = lo & mask;
+    while (top >= 0) {
+        const int width = top + 1 < 8 ? top + 1 : 8;
+        const int shift = top + 1 - width;
+        const uint32_t dm = (1u << width) - 1u;
+        reinterpret_cast<uint4*>(h)[lane] = make_uint4(0u, 0u, 0u, 0u);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* other lanes' bins: no store forwarding */
+        for (int i = lane; i < m; i += 64) {
+            const uint32_t k = stage[i];
+            if ((k & mask) == prefix) atomicAdd(&h[(k >> shift) & dm], 1u);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the adds of every lane land before the reads */
+        const uint4 c = reinterpret_cast<const uint4*>(h)[lane]; /* bins 4 lane .. 4 lane + 3 */
+        const uint32_t sum = c.x + c.y + c.z + c.w;
+        const uint32_t incl = wave_scan_u32(sum);
+        const uint32_t excl = incl - sum;
+        const uint64_t hit = __ballot((uint32_t)r >= excl && (uint32_t)r < incl);
+        const int L = hit ? __ffsll((unsigned long long)hit) - 1 : 63; /* r < m: always hit */
+        uint32_t d = 4u * (uint32_t)lane, below = excl;
+        if ((uint32_t)r >= below + c.x) { below += c.x; ++d;
+            if ((uint32_t)r >= below + c.y) { below += c.y; ++d;
+                if ((uint32_t)r >= below + c.z) { below += c.z; ++d; } } }
+        d = (uint32_t)__builtin_amdgcn_readlane((int)d, L);
+        below = (uint32_t)__builtin_amdgcn_readlane((int)below, L);
+        prefix |= d << shift;
+        mask |= dm << shift;
+        r -= (int)below;
+        top = shift - 1;
+    }
+    return prefix;
+} /* a segment barrier counter whose wait timed out */
 
 __device__ __forceinline__ uint64_t wall_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
@@ -1199,13 +1254,37 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             }
         }
         for (int j = tid; j < RES_HBINS; j += CT) raw[j] = 0u;
-        for (int j = tid; j < NSUB_MAX; j += CT) lsub[j] = 0u;
+        for (int j = tid; j < RES_NSUB; j += CT) lsub[j] = 0u;
         if (first && tid == 0) { /* memory-side words: later adds come from other workgroups */
             stc(reinterpret_cast<unsigned long long*>(&res[sd.res].zero_count), 0ull);
             stc(&res[sd.res].path, 0);
         }
         __syncthreads();
         WTP_RPROBE(8);
+#if WTP_RES_P0 == 1
+        /* the non-sampling waves stream at once; the sampling waves histogram their sample first
+         * (it comes back ahead of the flood) and issue their chunk after */
+        if (wv >= RES_SW) {
+            if (FULL) load_chunk<IT, CT>(sd.data + base, v);
+            else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
+        } else {
+#pragma unroll
+            for (int j = 0; j < RES_SPL; ++j)
+                if (j * (64 * RES_SW) + tid < m) atomicAdd(&raw[key_bin(ks[j])], 1u);
+        }
+        __syncthreads();
+        if (wv == 0) {
+            uint32_t wkl, wkh, wsh;
+            window_search_flat(sd, raw, m, exact, &wkl, &wkh, &wsh, t.pad[1] * 0.01, 8.0);
+            if (lane == 0) { s_win[0] = wkl; s_win[1] = wkh; s_win[2] = wsh; }
+            WTP_RPROBE(1);
+        }
+        if (wv < RES_SW) {
+            if (FULL) load_chunk<IT, CT>(sd.data + base, v);
+            else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
+        }
+        WTP_RPROBE(10);
+#else
         if (FULL) load_chunk<IT, CT>(sd.data + base, v);
         else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
         WTP_RPROBE(10);
@@ -1221,33 +1300,48 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             if (lane == 0) { s_win[0] = wkl; s_win[1] = wkh; s_win[2] = wsh; }
             WTP_RPROBE(1);
         }
+#endif
     }
     __syncthreads();
     const uint32_t kl = s_win[0], kh = s_win[1], sh = s_win[2];
-    /* ---- P1: one branch-free pass over the registers: counters, and the keys inside (kl, kh]
-     * appended to the thread's own LDS column (slot j of thread t at col[j * CT]; every key is
-     * written to the next free slot and kept only if inside -- no branch, no atomic).  Slots
-     * past len were loaded as +0.0: never inside, and the block totals drop them once. */
+    /* ---- P1: one branch-free pass over the registers: per key a compare for "below" (k < kl) and
+     * one for "== kl", counted on the scalar unit (ballot popcounts, wave totals directly), the
+     * max key, and the keys inside (kl, kh] appended to the thread's own LDS column (slot j of
+     * thread t at col[j * CT]; every key is written to the next free slot and kept only if inside
+     * -- no branch, no atomic).  Slots past len were loaded as +0.0: never inside, and the block
+     * totals drop them once. */
     const uint32_t span = kh - kl; /* >= 1 */
-    uint32_t below = 0, eql = 0, mx = 0, cnt = 0;
+    const uint32_t kl1 = kl + 1u;
+    uint32_t wbelow = 0, weql = 0, mx = 0, cnt = 0;
     uint32_t* col = wstage + tid;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
+        uint32_t k4[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) k4[c] = abs_key(opaque(f4_get(v[it], c)));
+        mx = max(mx, max(max(k4[0], k4[1]), max(k4[2], k4[3])));
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const uint32_t k = abs_key(opaque(f4_get(v[it], c)));
+            const uint32_t k = k4[c];
+#if WTP_RES_CNT == 1
+            wbelow += (uint32_t)__popcll(__ballot(k < kl));
+            weql += (uint32_t)__popcll(__ballot(k == kl));
+#else
             const uint32_t d = k - kl; /* keys and kl < 2^31: bit 31 set iff k < kl */
-            mx = max(mx, k);
-            below += d >> 31;
-            eql += d == 0u;
+            wbelow += d >> 31;
+            weql += d == 0u;
+#endif
             col[min(cnt, (uint32_t)RES_STG) * CT] = k;
-            cnt += d - 1u < span;
+            cnt += k - kl1 < span;
         }
     }
     {
-        const uint32_t r0 = wave_sum_u32(below), r1 = wave_sum_u32(eql), r2 = wave_max_u32(mx),
-                       r4 = wave_max_u32(cnt);
-        if (lane == 0) { wred[wv][0] = r0; wred[wv][1] = r1; wred[wv][2] = r2; wred[wv][5] = r4; }
+#if WTP_RES_CNT != 1
+        wbelow = wave_sum_u32(wbelow);
+        weql = wave_sum_u32(weql);
+#endif
+        const uint32_t r2 = wave_max_u32(mx), r4 = wave_max_u32(cnt);
+        if (lane == 0) { wred[wv][0] = wbelow; wred[wv][1] = weql; wred[wv][2] = r2; wred[wv][5] = r4; }
     }
     __syncthreads();
     WTP_RPROBE(2);
@@ -1270,6 +1364,8 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     }
     /* the inside keys' bucket histogram in LDS (eight column reads in flight per step), then the
      * segment's bucket totals as no-return atomic adds */
+    constexpr int BPT = RES_NSUB / CT; /* buckets per thread */
+    static_assert(BPT * CT == RES_NSUB, "buckets per thread");
     if (!ovf) { /* block-uniform */
         for (uint32_t j0 = 0; j0 < cnt; j0 += 8) {
             uint32_t kk[8];
@@ -1277,13 +1373,14 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             for (int u = 0; u < 8; ++u) kk[u] = col[min(j0 + u, (uint32_t)RES_STG) * CT];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                if (j0 + u < cnt) atomicAdd(&lsub[(kk[u] - kl - 1u) >> sh], 1u);
+                if (j0 + u < cnt) atomicAdd(&lsub[(kk[u] - kl1) >> sh], 1u);
         }
         __syncthreads();
-        static_assert(NSUB_MAX == 2 * CT, "two buckets per thread");
-        const uint32_t c0 = lsub[2 * tid], c1 = lsub[2 * tid + 1];
-        if (c0) atomicAdd(&st->sub[2 * tid], c0);
-        if (c1) atomicAdd(&st->sub[2 * tid + 1], c1);
+#pragma unroll
+        for (int j = 0; j < BPT; ++j) { /* bucket j * CT + tid: 256 contiguous bytes per wave instruction */
+            const uint32_t c = lsub[j * CT + tid];
+            if (c) atomicAdd(&st->sub[j * CT + tid], c);
+        }
     }
     WTP_RPROBE(3);
     /* ---- segment barrier 1: every workgroup's counters and bucket totals are in */
@@ -1330,8 +1427,12 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         }
         if (tid < 2) { s_bk[tid] = -1; s_bef[tid] = 0; s_bn[tid] = 0; }
     }
-    const uint32_t c0 = ldc<true>(st->sub + 2 * tid), c1 = ldc<true>(st->sub + 2 * tid + 1);
-    const uint32_t cs = c0 + c1;
+    uint32_t cb8[BPT]; /* buckets BPT * tid .. + BPT - 1, every load in flight before any is used */
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) cb8[j] = ldc<true>(st->sub + BPT * tid + j);
+    uint32_t cs = 0;
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) cs += cb8[j];
     const uint32_t incl = wave_scan_u32(cs);
     if (lane == 63) s_wtot[wv] = incl;
     __syncthreads();
@@ -1357,10 +1458,17 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     for (int i = 0; i < 2; ++i) {
         const int64_t j = i == 0 ? ja : jb;
         if ((i == 0 ? ca : cb) == 2 && j >= (int64_t)excl && j < (int64_t)(excl + cs)) {
-            const bool lo = j < (int64_t)(excl + c0);
-            s_bk[i] = 2 * tid + (lo ? 0 : 1);
-            s_bef[i] = lo ? excl : excl + c0;
-            s_bn[i] = lo ? c0 : c1;
+            uint32_t e = excl;
+            int b = BPT * tid;
+#pragma unroll
+            for (int u = 0; u < BPT - 1; ++u) {
+                const bool past = j >= (int64_t)(e + cb8[u]) && b == BPT * tid + u;
+                e += past ? cb8[u] : 0u;
+                b += past ? 1 : 0;
+            }
+            s_bk[i] = b;
+            s_bef[i] = e;
+            s_bn[i] = cb8[b - BPT * tid];
         }
     }
     __syncthreads();
@@ -1390,7 +1498,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 for (int u = 0; u < 8; ++u) kk[u] = col[min(j0 + u, (uint32_t)RES_STG) * CT];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
-                    const int bk = (int)((kk[u] - kl - 1u) >> sh);
+                    const int bk = (int)((kk[u] - kl1) >> sh);
                     if (j0 + u < cnt && (bk == ba || bk == bb)) {
                         const uint32_t p = atomicAdd(&s_fill, 1u);
                         if (p < (uint32_t)RES_SLOT_CAP) stc(slot + 1 + p, kk[u]);
@@ -1460,8 +1568,22 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 const uint32_t lo = (uint32_t)((uint64_t)kl + 1 + ((uint64_t)ba << sh));
                 const uint32_t hi = (uint32_t)min((uint64_t)kh, (uint64_t)kl + ((uint64_t)(bb + 1) << sh));
                 uint32_t xa = kl, xb = kl;
-                select_in_range<CT>([&](int64_t i) { return stage[i]; }, [](uint32_t) { return true; }, (int64_t)m, lo,
-                                    hi, ja - (int64_t)before, jb - (int64_t)before, ca == 2, cb == 2, &xa, &xb);
+#if WTP_RES_FSEL == 0
+                select_in_range<CT>([&](int64_t i) { return stage[i]; }, [](uint32_t) { return true; }, (int64_t)m,
+                                    lo, hi, ja - (int64_t)before, jb - (int64_t)before, ca == 2, cb == 2, &xa, &xb);
+#else
+                { /* wave 0 takes r0, wave 1 takes r1: one-wave radix selects over private histograms */
+                    __shared__ uint32_t s_x[2];
+                    if (wv < 2 && (wv == 0 ? ca : cb) == 2) {
+                        const int r = (int)((wv == 0 ? ja : jb) - (int64_t)before);
+                        const uint32_t k = wave_radix_select(stage, m, r, lo, hi, raw + RES_SEL_MAX + 256 * wv);
+                        if (lane == 0) s_x[wv] = k;
+                    }
+                    __syncthreads();
+                    xa = s_x[0];
+                    xb = s_x[1];
+                }
+#endif
                 ka = ca == 2 ? xa : kl;
                 kb = cb == 2 ? xb : kl;
                 path = MODE_CAND;
@@ -1534,7 +1656,13 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         for (int it = 0; it < IT; ++it) {
             float4 y;
             y.x = fin(v[it].x); y.y = fin(v[it].y); y.z = fin(v[it].z); y.w = fin(v[it].w);
+#if WTP_RES_NTST
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v yv = {y.x, y.y, y.z, y.w};
+            __builtin_nontemporal_store(yv, reinterpret_cast<f4v*>(q4 + it * CT + tid));
+#else
             q4[it * CT + tid] = y;
+#endif
         }
     } else {
         const __amdgpu_buffer_rsrc_t rr = ragged_rsrc(qo, len);
@@ -1562,7 +1690,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader*
                                                           uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
                                                           float* __restrict__ thr_out) {
     __shared__ __attribute__((aligned(16))) uint32_t raw[RES_HBINS > RES_SEL_MAX ? RES_HBINS : RES_SEL_MAX];
-    __shared__ uint32_t lsub[NSUB_MAX];
+    __shared__ uint32_t lsub[RES_NSUB];
     __shared__ uint32_t wred[RES_THREADS / 64][8];
     __shared__ uint32_t wstage[(RES_STG + 1) * RES_THREADS]; /* 66 KB: RES_STG slots + the discard slot per thread */
     const uint32_t q = head->parity;

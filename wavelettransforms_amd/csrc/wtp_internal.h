@@ -26,6 +26,8 @@ constexpr int M_SAMPLE_WIN = 16384; /* k_window (three-launch form): one block p
                                        narrower window halves k_collect's candidate traffic */
 constexpr int SAMPLE_GROUP = 16;   /* contiguous keys per sample group */
 constexpr int NSUB_MAX = 1024;     /* buckets over (kl, kh]: 64..1024 per segment (SegDesc) */
+constexpr int RES_NSUB_LOG2 = 10;  /* k_resident: 1024 buckets over (kl, kh] (4096 measured slower: 8 KB more reads per workgroup) */
+constexpr int RES_NSUB = 1 << RES_NSUB_LOG2;
 constexpr int BUCKET_MAX = 8192;   /* keys per bucket (two buckets are staged in LDS)       */
 constexpr int BUCKET_MAX_DWT = 1 << 16; /* DWT segments: 64 wide buckets, one select per segment */
 constexpr int WIN_EXP = 32;
@@ -121,9 +123,9 @@ struct alignas(128) SelState {
     float thr32;                      /* the float32 threshold the compare uses              */
     uint32_t key_a, key_b;            /* resolved order statistics                           */
     uint32_t pad1[25];
-    uint32_t sub[NSUB_MAX];           /* keys per bucket (returning atomicAdd, k_collect)    */
+    uint32_t sub[RES_NSUB];           /* keys per bucket (atomicAdd; k_collect uses <= NSUB_MAX) */
 };
-static_assert(sizeof(SelState) % 128 == 0 && sizeof(SelState) == 4608, "SelState layout");
+static_assert(sizeof(SelState) % 128 == 0 && sizeof(SelState) == 512 + 4 * RES_NSUB, "SelState layout");
 
 /* The persistent head of a workspace: two SelState regions used alternately by successive
  * launch groups.  A group's k_collect accumulates into region `parity`, zeroes the other
