@@ -1303,16 +1303,20 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
 #endif
     }
     __syncthreads();
-    const uint32_t kl = s_win[0], kh = s_win[1], sh = s_win[2];
-    /* ---- P1: one branch-free pass over the registers: per key a compare for "below" (k < kl) and
-     * one for "== kl", counted on the scalar unit (ballot popcounts, wave totals directly), the
-     * max key, and the keys inside (kl, kh] appended to the thread's own LDS column (slot j of
-     * thread t at col[j * CT]; every key is written to the next free slot and kept only if inside
-     * -- no branch, no atomic).  Slots past len were loaded as +0.0: never inside, and the block
-     * totals drop them once. */
+    const uint32_t kl = s_win[0], kh = s_win[1];
+    /* ---- P1: one branch-free pass over the registers, two classes per key from one difference
+     * d = k - kl (keys and kl < 2^31): "below" (k < kl: bit 31 of d) and "inside" [kl, kh]
+     * (d <= span; keys == kl belong to bucket 0), the max key, and the inside keys appended to the
+     * thread's own LDS column (slot j of thread t at col[j * CT]; every key is written to the next
+     * free slot and kept only if inside -- no branch, no atomic).  In a ragged chunk the slots
+     * past len were loaded as +0.0: never inside, counted below (kl > 0) and dropped once. */
     const uint32_t span = kh - kl; /* >= 1 */
-    const uint32_t kl1 = kl + 1u;
-    uint32_t wbelow = 0, weql = 0, mx = 0, cnt = 0;
+    uint32_t sh = 0; /* bucket of an inside key: (k - kl) >> sh, RES_NSUB buckets */
+    if (span > 0) {
+        const int bits = 32 - __clz(span);
+        sh = bits > RES_NSUB_LOG2 ? bits - RES_NSUB_LOG2 : 0;
+    }
+    uint32_t wbelow = 0, mx = 0, cnt = 0;
     uint32_t* col = wstage + tid;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
@@ -1323,25 +1327,17 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const uint32_t k = k4[c];
-#if WTP_RES_CNT == 1
-            wbelow += (uint32_t)__popcll(__ballot(k < kl));
-            weql += (uint32_t)__popcll(__ballot(k == kl));
-#else
-            const uint32_t d = k - kl; /* keys and kl < 2^31: bit 31 set iff k < kl */
+            const uint32_t d = k - kl;
             wbelow += d >> 31;
-            weql += d == 0u;
-#endif
             col[min(cnt, (uint32_t)RES_STG) * CT] = k;
-            cnt += k - kl1 < span;
+            const bool valid = FULL || 4 * (it * CT + tid) + c < len;
+            cnt += (d <= span) & valid;
         }
     }
     {
-#if WTP_RES_CNT != 1
         wbelow = wave_sum_u32(wbelow);
-        weql = wave_sum_u32(weql);
-#endif
         const uint32_t r2 = wave_max_u32(mx), r4 = wave_max_u32(cnt);
-        if (lane == 0) { wred[wv][0] = wbelow; wred[wv][1] = weql; wred[wv][2] = r2; wred[wv][5] = r4; }
+        if (lane == 0) { wred[wv][0] = wbelow; wred[wv][2] = r2; wred[wv][5] = r4; }
     }
     __syncthreads();
     WTP_RPROBE(2);
@@ -1351,14 +1347,12 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     /* block-uniform: a thread's column overflowed -> the segment takes the full scan */
     const bool ovf = wmax > (uint32_t)RES_STG;
     if (tid == 0) {
-        unsigned long long a0 = 0, a1 = 0;
+        unsigned long long a0 = 0;
         uint32_t m2 = 0;
-        for (int w = 0; w < NW; ++w) { a0 += wred[w][0]; a1 += wred[w][1]; m2 = max(m2, wred[w][2]); }
-        const unsigned long long pad = (unsigned long long)(RES_CHUNK - len);
-        if (kl > 0) a0 -= pad; else a1 -= pad;
+        for (int w = 0; w < NW; ++w) { a0 += wred[w][0]; m2 = max(m2, wred[w][2]); }
+        if (kl > 0) a0 -= (unsigned long long)(RES_CHUNK - len);
         const int sh8 = blockIdx.x & (NSHARD - 1);
         if (a0) atomicAdd(&st->below[sh8], a0);
-        if (a1) atomicAdd(&st->eq_lo[sh8], a1);
         atomicMax(&st->maxkey[sh8], m2);
         if (ovf) atomicOr(&st->overflow, 1u);
     }
@@ -1373,7 +1367,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             for (int u = 0; u < 8; ++u) kk[u] = col[min(j0 + u, (uint32_t)RES_STG) * CT];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                if (j0 + u < cnt) atomicAdd(&lsub[(kk[u] - kl1) >> sh], 1u);
+                if (j0 + u < cnt) atomicAdd(&lsub[(kk[u] - kl) >> sh], 1u);
         }
         __syncthreads();
 #pragma unroll
@@ -1400,20 +1394,19 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     WTP_RPROBE(5);
     /* ---- P2: the segment's counters and bucket totals in one round trip (every load in
      * flight before any is used); a block scan of the totals names the bucket of each rank */
-    __shared__ unsigned long long s_cnt[2];
+    __shared__ unsigned long long s_cnt[1];
     __shared__ uint32_t s_mk, s_ovf, s_wtot[NW];
     __shared__ int s_bk[2];
     __shared__ uint32_t s_bef[2], s_bn[2];
     {
-        if (tid < 2) {
-            const unsigned long long* a = tid == 0 ? st->below : st->eq_lo;
+        if (tid == 0) {
             unsigned long long x[NSHARD];
 #pragma unroll
-            for (int i = 0; i < NSHARD; ++i) x[i] = ldc<true>(a + i);
+            for (int i = 0; i < NSHARD; ++i) x[i] = ldc<true>(st->below + i);
             unsigned long long sum = 0;
 #pragma unroll
             for (int i = 0; i < NSHARD; ++i) sum += x[i];
-            s_cnt[tid] = sum;
+            s_cnt[0] = sum;
         } else if (tid == 2) {
             uint32_t x[NSHARD];
 #pragma unroll
@@ -1437,18 +1430,16 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     if (lane == 63) s_wtot[wv] = incl;
     __syncthreads();
     WTP_PROBE(1);
-    const int64_t sbelow = (int64_t)s_cnt[0], seql = (int64_t)s_cnt[1];
+    const int64_t sbelow = (int64_t)s_cnt[0];
     const uint32_t mk = s_mk;
     uint32_t excl = incl - cs, ninside = 0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) { const uint32_t x = s_wtot[w]; ninside += x; excl += w < wv ? x : 0u; }
     const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
-    /* class of a rank: 0 outside the window, 1 == kl, 2 inside (kl, kh] at inside-rank j */
+    /* class of a rank: 0 outside the window, 2 inside [kl, kh] at inside-rank j */
     auto classify = [&](int64_t r, int64_t* j) {
         if (r < sbelow) return 0;
         r -= sbelow;
-        if (r < seql) return 1;
-        r -= seql;
         if (r < (int64_t)ninside) { *j = r; return 2; }
         return 0;
     };
@@ -1498,7 +1489,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 for (int u = 0; u < 8; ++u) kk[u] = col[min(j0 + u, (uint32_t)RES_STG) * CT];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
-                    const int bk = (int)((kk[u] - kl1) >> sh);
+                    const int bk = (int)((kk[u] - kl) >> sh);
                     if (j0 + u < cnt && (bk == ba || bk == bb)) {
                         const uint32_t p = atomicAdd(&s_fill, 1u);
                         if (p < (uint32_t)RES_SLOT_CAP) stc(slot + 1 + p, kk[u]);
@@ -1565,8 +1556,8 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 WTP_PROBE(5);
                 /* ---- the ranks among the staged keys (buckets ba..bb; buckets between are empty:
                  * the two ranks are adjacent): an LDS radix select of both at once */
-                const uint32_t lo = (uint32_t)((uint64_t)kl + 1 + ((uint64_t)ba << sh));
-                const uint32_t hi = (uint32_t)min((uint64_t)kh, (uint64_t)kl + ((uint64_t)(bb + 1) << sh));
+                const uint32_t lo = (uint32_t)((uint64_t)kl + ((uint64_t)ba << sh));
+                const uint32_t hi = (uint32_t)min((uint64_t)kh, (uint64_t)kl + ((uint64_t)(bb + 1) << sh) - 1);
                 uint32_t xa = kl, xb = kl;
 #if WTP_RES_FSEL == 0
                 select_in_range<CT>([&](int64_t i) { return stage[i]; }, [](uint32_t) { return true; }, (int64_t)m,
@@ -1610,7 +1601,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     if (first) {
         /* zeros of where(|x| < thr, 0, x) = #(key < tk), tk = bits(thr) when thr > 0, else 1 (only
          * the zeros themselves); ka <= thr <= kb and the ranks are adjacent, so #(key < tk) =
-         * below + [tk > kl] eq + before + #(staged < tk).  A NaN threshold prunes nothing: every
+         * below + before + #(staged < tk).  A NaN threshold prunes nothing: every
          * workgroup counts the zeros of its copy below. */
         unsigned long long zc = 0;
         if (!nan) {
@@ -1622,7 +1613,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 if (path == MODE_CAND)
                     for (int i = tid; i < m; i += CT) c += stage[i] < tk;
                 const unsigned long long sc = block_sum_u64<CT>(c);
-                zc = (unsigned long long)sbelow + (tk > kl ? (unsigned long long)seql : 0ull) +
+                zc = (unsigned long long)sbelow +
                      (path == MODE_CAND ? (unsigned long long)before : 0ull) + sc;
             }
         }
