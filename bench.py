@@ -112,7 +112,10 @@ def rocprof_child(args, timeout=240):
     d = tempfile.mkdtemp(prefix="wtp_bench_prof_", dir="/tmp")
     cmd = [prof, "--kernel-trace", "--stats", "-d", d, "-o", "run", "--output-format", "csv", "--",
            sys.executable, os.path.abspath(__file__), "--profile-child", "--config", args.config,
-           "--steps", str(max(args.steps, 200)), "--warmup", str(args.warmup), "--blocks", str(args.blocks)]
+           "--steps", str(max(args.steps, 200)), "--warmup", str(args.warmup), "--blocks", str(args.blocks),
+           "--graph-steps", str(args.graph_steps)]
+    if args.no_graph:
+        cmd.append("--no-graph")
     if args.flatten:
         cmd.append("--flatten")
     if args.no_resident:
@@ -133,16 +136,24 @@ def rocprof_child(args, timeout=240):
         shutil.rmtree(d, ignore_errors=True)
 
 
-def rocprof_avg_us(stats, kernel):
-    """Average duration (us) over every launch of the wtp kernel named `kernel` (any template
-    instance) in a rocprof_child summary; (None, 0) if absent."""
+def rocprof_kernel(stats, kernel):
+    """(total ns, launches) of the wtp kernel named `kernel` (every template instance) in a
+    rocprof_child summary; (0.0, 0) if absent."""
     calls, total = 0, 0.0
     for name, (c, t) in (stats or {}).items():
         base = name.split("(")[0].split("<")[0].replace("void ", "").strip()
         if base == "wtp::" + kernel:
             calls += c
             total += t
-    return (total / calls * 1e-3, calls) if calls else (None, 0)
+    return total, calls
+
+
+def child_steps(args):
+    """Steps the rocprof child executes: warmup, the side-stream step and two warm replays of the
+    graph (when one is captured), then the timed steps."""
+    K = max(args.steps, 200)
+    G = max(1, min(args.graph_steps, K))
+    return args.warmup + K + (0 if args.no_graph else 1 + 2 * G)
 
 
 def cpu_model():
@@ -396,14 +407,17 @@ def main():
         dom_us = ms_per_step * 1e3
     traffic, traffic_src, traffic_tag = pmc_traffic(args.config, dom_kernel) if dom else (None, None, None)
     stamps_us = dom_us if dom == "k_resident" else None
-    prof_us, prof_calls = rocprof_avg_us(prof_stats, dom_kernel) if dom else (None, 0)
-    if prof_us is not None:
-        # the launch duration rocprofv3 records for the dominant kernel in the child run of this
-        # configuration (dispatch to completion, what profiles/ summaries hold); per stage:
-        # launches_per_stage x the average
-        dom_us = prof_us * dom_launches
+    prof_ns, prof_calls = rocprof_kernel(prof_stats, dom_kernel) if dom else (0.0, 0)
+    if prof_calls:
+        # the durations rocprofv3 records for the dominant kernel in the child run of this
+        # configuration (dispatch to completion, what profiles/ summaries hold), per step: a
+        # stage's launches (levels x image groups) summed
+        nsteps = child_steps(args)
+        dom_launches = prof_calls / nsteps
+        dom_us = prof_ns / nsteps * 1e-3
         timing_src = ("rocprofv3 --kernel-trace --stats of this configuration's step loop, run as a child of "
-                      "this bench (%d launches of %s, average)" % (prof_calls, dom_kernel))
+                      "this bench: %d launches of %s over %d steps, device time per step"
+                      % (prof_calls, dom_kernel, nsteps))
 
     # ------------------------------------------------ cold Infinity Cache (MALL)
     cold = None
