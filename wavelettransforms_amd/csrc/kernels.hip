@@ -197,6 +197,9 @@ __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, i
 #ifndef WTP_RES_CNT /* k_resident's below / == kl counts: 1 ballot popcounts (scalar unit), 0 per-lane */
 #define WTP_RES_CNT 0
 #endif
+#ifndef WTP_RES_SPEC /* k_resident: speculative stores of the decided keys during the second barrier */
+#define WTP_RES_SPEC 0
+#endif
 #ifndef WTP_RES_NTST /* k_resident's output stores: 1 nontemporal (tools/mb/reslab.hip A/B) */
 #define WTP_RES_NTST 1
 #endif
@@ -1465,6 +1468,8 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     __syncthreads();
     WTP_PROBE(2);
     bool full = ca == 0 || cb == 0 || s_ovf != 0;
+    bool specd = false;   /* this workgroup's chunk was stored speculatively */
+    uint32_t spec_lo = 0; /* keys below it were stored pruned, the rest unpruned */
     int path = MODE_WINDOW;
     uint32_t ka = kl, kb = kl;
     uint32_t before = 0;
@@ -1501,6 +1506,25 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             /* ---- segment barrier 2: every slot of the segment is written */
             res_arrive(b2);
             WTP_PROBE(3);
+#if WTP_RES_SPEC
+            /* speculative stores while the segment's slots come in (out of place only: a segment
+             * that still falls back to the full scan re-reads its intact input; never with inf /
+             * NaN keys): every key outside buckets ba..bb is decided -- below them pruned, above
+             * them kept -- and the undecided ones are written unpruned and fixed after the select */
+            if (FULL && sd.out != sd.data && mk < 0x7F800000u) {
+                const uint32_t ulo = (uint32_t)((uint64_t)kl + ((uint64_t)ba << sh));
+                float4* q4 = reinterpret_cast<float4*>(sd.out + base);
+                typedef float f4v __attribute__((ext_vector_type(4)));
+                auto g = [&](float xv) { return abs_key(xv) < ulo ? 0.0f : xv; };
+#pragma unroll
+                for (int it = 0; it < IT; ++it) {
+                    const f4v yv = {g(v[it].x), g(v[it].y), g(v[it].z), g(v[it].w)};
+                    __builtin_nontemporal_store(yv, reinterpret_cast<f4v*>(q4 + it * CT + tid));
+                }
+                specd = true;
+                spec_lo = ulo;
+            }
+#endif
             if (!res_wait(b2, nwg, tmo)) {
                 if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
                 return;
@@ -1641,7 +1665,18 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     /* ---- P3: out = where(|x| < thr, 0, x) from registers (a NaN threshold prunes nothing) */
     float* qo = sd.out + base;
     auto fin = [&](float xv) { return (fabsf(xv) < thr) ? 0.0f : xv; };
-    if (FULL) {
+    if (specd && path == MODE_CAND && !nan) {
+        /* only the keys the speculative store left unpruned that the threshold prunes: one
+         * dword each (a few per workgroup) */
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float xv = f4_get(v[it], c);
+                if (abs_key(xv) >= spec_lo && fabsf(xv) < thr) qo[4 * (it * CT + tid) + c] = 0.0f;
+            }
+        }
+    } else if (FULL) {
         float4* q4 = reinterpret_cast<float4*>(qo);
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
