@@ -61,7 +61,8 @@ typedef struct wtp_result {
     uint32_t thr32_bits;    /* float32(thr64): the compare of :31 runs in float32    */
     uint32_t max_abs_bits;  /* np.max(np.abs(coeff_arr)) as float32 bits  :29-30     */
     int32_t eff_level;      /* min(level, calculate_max_level(shape))     :64-65     */
-    int32_t path;           /* selection: 1 window candidates, 2 window edges, 3 full scan;
+    int32_t path;           /* selection: 1 window candidates, 2 window edges, 3 full scan,
+                               4 the one-launch small path (exact three-digit radix select);
                                99 = the resident launch's grid was not co-resident (results invalid) */
 } wtp_result;
 
@@ -178,6 +179,7 @@ int wtp_resident_capacity(void); /* 0 if the current device cannot host the resi
  * Default 200000; tests lower it to force the fault path. */
 unsigned wtp_set_resident_timeout_us(unsigned us);
 #define WTP_PATH_FAULT 99
+#define WTP_PATH_SMALL 4 /* every tensor of the call ran in one launch (2-D transforms, small population) */
 /* measurement hook (bench.py): while set, every resident launch atomically lowers stamps_dev[0] to
  * its first workgroup's start and raises stamps_dev[1] to its last workgroup's end (after that
  * workgroup's stores completed), in ticks of the 100 MHz wall clock -- the launch's span on the

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "wtp_internal.h"
+#include "small_geom.h"
 #include "wt_filters.inc"
 #include "wt_perm.h"
 
@@ -354,6 +355,133 @@ void inverse_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s)
     }
 }
 
+/* ---- the one-launch small path (small.hip) ---- */
+constexpr int64_t SM_POP_MAX = 1 << 20; /* population of a whole call taken by k_small */
+constexpr int SM_TILES_MAX = 64;        /* workgroups per tensor */
+
+/* Tile sizes (TR x TC at level L) for one tensor: every tile's forward and inverse arena must
+ * fit; among those, the least per-workgroup level-0 window plus a charge per workgroup. */
+bool small_tiling(const TPlan& p, int F, int budget, int words, SmallSeg& sg) {
+    const int L = p.L;
+    int32_t Rn[SM_LMAX + 1], Cn[SM_LMAX + 1];
+    for (int k = 0; k <= L; ++k) { Rn[k] = (int32_t)p.g.R[k]; Cn[k] = (int32_t)p.g.C[k]; }
+    const int RL = Rn[L], CL = Cn[L];
+    int64_t best = INT64_MAX;
+    std::vector<SmAxis> ar, ac;
+    for (int TR = RL;; TR = (TR + 1) / 2) {
+        const int tR = (RL + TR - 1) / TR;
+        ar.resize(tR);
+        for (int i = 0; i < tR; ++i) sm_axis(i, TR, L, Rn, F, &ar[i]);
+        for (int TC = CL;; TC = (TC + 1) / 2) {
+            const int tC = (CL + TC - 1) / TC;
+            const int64_t tiles = p.B * tR * tC;
+            if (tiles <= budget && 3 * (L + 1) * (tR + tC) <= words) {
+                ac.resize(tC);
+                for (int j = 0; j < tC; ++j) sm_axis(j, TC, L, Cn, F, &ac[j]);
+                int64_t worst = 0;
+                bool fits = true;
+                for (int i = 0; i < tR && fits; ++i)
+                    for (int j = 0; j < tC && fits; ++j) {
+                        const SmNeed nd = sm_need(ar[i], ac[j], L, F);
+                        fits = sm_fwd_words(nd) <= SM_ARENA && sm_inv_words(nd) <= SM_ARENA;
+                        worst = std::max<int64_t>(worst, (int64_t)ar[i].fw[0].len * ac[j].fw[0].len + nd.fkeys / 2);
+                    }
+                const int64_t cost = worst + 64 * tiles;
+                if (fits && cost < best) {
+                    best = cost;
+                    sg.TR = TR;
+                    sg.TC = TC;
+                    sg.tilesR = tR;
+                    sg.tilesC = tC;
+                }
+            }
+            if (TC == 1) break;
+        }
+        if (TR == 1) break;
+    }
+    return best != INT64_MAX;
+}
+
+/* k_small takes the whole call when every tensor is a 2-D transform, the call is small and
+ * every tensor finds a tiling inside the co-resident grid */
+bool plan_small(const std::vector<TPlan>& ps, const wtp_tensor* ts, int n, void* ws, double pct, const Taps& tp,
+                SmallTable& t) {
+    if (n > SM_MAX_SEG || (tp.F & 1) || tp.F < 2 || tp.F > SM_F_MAX) return false;
+    const int cap = std::min(resident_capacity(), RES_MAX_WG);
+    int64_t tot = 0;
+    for (const TPlan& p : ps) {
+        if (!p.dwt || p.flat || p.L > SM_LMAX || p.H > SM_LINE_MAX || p.W > SM_LINE_MAX) return false;
+        tot += p.pop;
+    }
+    if (tot > SM_POP_MAX || cap < n) return false;
+    memset(&t, 0, sizeof t);
+    int wg = 0, words = 0;
+    for (int i = 0; i < n; ++i) {
+        const TPlan& p = ps[i];
+        SmallSeg& sg = t.s[i];
+        static const int tiles_max = [] { /* lab knob: workgroups per tensor */
+            const char* e = getenv("WTP_SM_TILES");
+            return e && atoi(e) > 0 ? atoi(e) : SM_TILES_MAX;
+        }();
+        /* workgroups by share of the population, at least one per image */
+        const int budget = (int)std::max<int64_t>(p.B, std::min<int64_t>(tiles_max, (int64_t)cap * p.pop / tot));
+        if (!small_tiling(p, tp.F, budget, (SM_WIN_WORDS - words) / (n - i), sg)) return false;
+        /* the windows of every tile row and tile column, packed (small_geom.h computes them) */
+        {
+            int32_t Rn[SM_LMAX + 1], Cn[SM_LMAX + 1];
+            for (int k = 0; k <= p.L; ++k) { Rn[k] = (int32_t)p.g.R[k]; Cn[k] = (int32_t)p.g.C[k]; }
+            sg.win_off = words;
+            auto pack = [&](const SmAxis& a) {
+                for (int k = 0; k <= p.L; ++k) {
+                    t.win[words++] = (uint32_t)a.fw[k].s | ((uint32_t)a.fw[k].len << 16);
+                    t.win[words++] = (uint32_t)a.sv[k].s | ((uint32_t)a.sv[k].len << 16);
+                    t.win[words++] = (uint32_t)a.olo[k] | ((uint32_t)a.ohi[k] << 16);
+                }
+            };
+            SmAxis a;
+            for (int r = 0; r < sg.tilesR; ++r) { sm_axis(r, sg.TR, p.L, Rn, tp.F, &a); pack(a); }
+            for (int c = 0; c < sg.tilesC; ++c) { sm_axis(c, sg.TC, p.L, Cn, tp.F, &a); pack(a); }
+        }
+        sg.in = ts[i].in;
+        sg.out = ts[i].out;
+        sg.P = reinterpret_cast<float*>(wsb(ws, p.p_off));
+        SegDesc sd;
+        memset(&sd, 0, sizeof sd);
+        seg_ranks(p.pop, pct, sd);
+        sg.r0 = sd.r0;
+        sg.gamma = sd.gamma;
+        sg.above = sd.above;
+        sg.numel = p.numel;
+        sg.n = p.pop;
+        sg.B = (int32_t)p.B;
+        sg.L = p.L;
+        sg.PR = (int32_t)p.g.PR;
+        sg.PC = (int32_t)p.g.PC;
+        int64_t nc = p.g.R[p.L] * p.g.C[p.L];
+        for (int k = 0; k <= p.L; ++k) {
+            sg.R[k] = (int32_t)p.g.R[k];
+            sg.C[k] = (int32_t)p.g.C[k];
+            sg.offR[k] = k ? (int32_t)p.g.offR[k] : 0;
+            sg.offC[k] = k ? (int32_t)p.g.offC[k] : 0;
+            if (k) nc += 3 * p.g.R[k] * p.g.C[k];
+        }
+        sg.npad = (int32_t)(p.pop - p.B * nc);
+        sg.res = i;
+        sg.wg_begin = wg;
+        sg.nwg = (int32_t)(p.B * sg.tilesR * sg.tilesC);
+        t.wg_begin[i] = wg;
+        wg += sg.nwg;
+    }
+    for (int i = n; i < SM_MAX_SEG; ++i) t.wg_begin[i] = INT32_MAX;
+    if (wg > cap) return false;
+    t.nseg = n;
+    t.nblk = wg;
+    t.tp.F = tp.F;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < SM_F_MAX; ++j) t.tp.f[i][j] = j < tp.F ? tp.f[i][j] : 0.0f;
+    return true;
+}
+
 /* pywt.wavedec / waverec (periodization) of one flattened tensor (1-D mode): packed layout
  * [cA_L | cD_L | cD_L-1 | ... | cD_1] (pywt.coeffs_to_array of a 1-D list) */
 int64_t flat_off_d(const TPlan& p, int k) {
@@ -466,6 +594,16 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     const Taps tp = (wavelet_id >= 0 && wavelet_id < WT_NUM_WAVELETS) ? make_taps(wavelet_id) : Taps{};
 
     stage(0, s);
+    if (!no_resident && !flat && g_resident.load(std::memory_order_relaxed)) {
+        /* a small call: the whole path in one launch (small.hip) */
+        SmallTable st;
+        if (plan_small(ps, tensors, ntensors, ws, pct, tp, st)) {
+            for (int i = 1; i <= 4; ++i) stage(i, s);
+            launch_small(st, head, results, s);
+            stage(5, s);
+            return check_launch();
+        }
+    }
     /* 1. forward transforms into the packed arrays (pywt.wavedec2 + coeffs_to_array) */
     std::vector<Chain> chains;
     for (int t = 0; t < ntensors; ++t) {

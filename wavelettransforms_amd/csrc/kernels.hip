@@ -1143,7 +1143,6 @@ __device__ __forceinline__ void window_search_flat(const SegDesc& sd, const uint
     *sh_out = sh;
 }
 
-constexpr uint32_t RES_POISON = 0x80000000u;
 
 /* Rank r (0-based, ascending) among the m keys stage[0..m), all in [lo, hi]: ONE wave, an MSB-first
  * radix select in 8-bit digits below the common prefix of lo and hi over a private 256-bin LDS
@@ -2187,6 +2186,8 @@ static std::atomic<uint32_t> g_res_timeout_us{RES_TIMEOUT_DEFAULT_US};
 uint32_t set_resident_timeout_us(uint32_t us) { return g_res_timeout_us.exchange(us); }
 static std::atomic<unsigned long long*> g_stamps{nullptr};
 void set_kernel_stamps(unsigned long long* dev) { g_stamps.store(dev); }
+uint32_t resident_timeout_us() { return g_res_timeout_us.load(std::memory_order_relaxed); }
+unsigned long long* kernel_stamps() { return g_stamps.load(std::memory_order_relaxed); }
 void launch_resident(const SegTable& t0, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
                      hipStream_t s) {
     static const int sig = [] { const char* e = getenv("WTP_RES_SIGMA"); return e && atoi(e) > 0 ? atoi(e) : RES_SIGMA_X100; }();

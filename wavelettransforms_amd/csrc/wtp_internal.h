@@ -200,9 +200,54 @@ constexpr int RES_SEL_MAX = 1024;                   /* keys the one-wave select 
 constexpr uint32_t RES_TIMEOUT_DEFAULT_US = 200000; /* a wait this long means the grid is not co-resident */
 int resident_capacity();
 uint32_t set_resident_timeout_us(uint32_t us); /* every k_resident wait's bound; returns the previous one */
-void set_kernel_stamps(unsigned long long* dev); /* k_resident launch span stamps (measurement) */                            /* co-resident workgroups on the current device */
+void set_kernel_stamps(unsigned long long* dev); /* k_resident / k_small launch span stamps (measurement) */
+uint32_t resident_timeout_us();
+unsigned long long* kernel_stamps();
+constexpr uint32_t RES_POISON = 0x80000000u; /* a segment barrier counter whose wait timed out */
 void launch_resident(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
                      hipStream_t s);
+/* ---- the small-population path in one launch (small.hip, k_small) ----
+ * every tensor of the call is a 2-D transform whose tiles fit one workgroup's LDS; one
+ * workgroup per tile, the tiles of a tensor are its segment (small_geom.h) */
+constexpr int SM_MAX_SEG = 6;       /* tensors per call */
+constexpr int SM_ARENA = 34 * 1024; /* LDS words of a workgroup's arena (136 KB) */
+constexpr int SM_F_MAX = 20;        /* longest filter */
+constexpr int SM_LMAX = 10;         /* = SM_MAX_L of small_geom.h */
+constexpr int SM_WIN_WORDS = 480;   /* the tiles' windows, computed by the host (small_geom.h): per tile row
+                                       and per tile column 3 (L + 1) words, level k's fw, sv and own range */
+constexpr int SM_LINE_MAX = 32767;  /* window ends packed in 16 bits */
+struct SmallSeg {
+    const float* in;
+    float* out;
+    float* P;         /* packed coefficients (workspace), B images of PR x PC */
+    int64_t r0;       /* lower order statistic of the population          */
+    double gamma;
+    int64_t numel;
+    int64_t n;        /* population: B * PR * PC                          */
+    int32_t B, L, PR, PC;
+    int32_t R[SM_LMAX + 1], C[SM_LMAX + 1], offR[SM_LMAX + 1], offC[SM_LMAX + 1];
+    int32_t TR, TC, tilesR, tilesC; /* tile size at level L, tiles per image  */
+    int32_t wg_begin, nwg, res, above, npad;
+    int32_t win_off; /* this tensor's lines in SmallTable::win: tilesR row lines, then tilesC column lines */
+};
+struct SmallTaps { /* the filter in the kernel argument: only as many taps as the path takes */
+    int32_t F;
+    int32_t pad[3];
+    float f[4][SM_F_MAX]; /* dec_lo, dec_hi, rec_lo, rec_hi */
+};
+struct SmallTable {
+    int32_t nseg, nblk;
+    uint32_t timeout; /* set by launch_small */
+    int32_t pad;
+    unsigned long long* stamps;
+    int32_t wg_begin[SM_MAX_SEG]; /* INT32_MAX past nseg */
+    SmallSeg s[SM_MAX_SEG];
+    SmallTaps tp;
+    uint32_t win[SM_WIN_WORDS];
+};
+static_assert(sizeof(SmallTable) <= 4096, "k_small's kernel argument");
+void launch_small(const SmallTable& t, SelHeader* head, wtp_result* res, hipStream_t s);
+
 /* min-weight pruning after window + collect: mp = 16 B per tensor, tiecnt = one u32 per
  * streaming block */
 void launch_minprune(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,

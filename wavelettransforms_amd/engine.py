@@ -164,6 +164,7 @@ def launch(tensors, wavelet, level, pct, outs=None, carry_level=True, stream=Non
 
 
 MODE_FAULT = 99  # WTP_PATH_FAULT: the resident launch timed out for this tensor and stored nothing
+MODE_SMALL = 4   # WTP_PATH_SMALL: the whole call ran as one launch (csrc/small.hip)
 
 
 def carried_level(tensors, wavelet, level, flatten=False):
