@@ -13,9 +13,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PROBE_LIB = os.path.join(ROOT, "tools", "mb", "libwtprune_probe.so")
-PHASES = [(6, "entry"), (0, "windows"), (1, "L0 loaded"), (2, "L1 col pass"), (3, "L1 row pass"), (4, "L2 col pass"),
-          (5, "L2 row pass"), (7, "L3 col pass"), (8, "L3 row pass"), (10, "arrived 0"), (11, "digit 1"),
-          (12, "digit 2"), (13, "digit 3"), (14, "I start"), (15, "stores drained")]
+PHASES = [(6, "entry"), (0, "windows"), (1, "L0 loaded"), (10, "arrived 0"), (11, "barrier 0"),
+          (2, "bin located"), (3, "slot written"), (4, "arrived 1"), (5, "barrier 1"), (7, "windows in LDS"),
+          (8, "slots in LDS"), (9, "slot headers"), (12, "pass A"), (13, "ranks"), (14, "I start"),
+          (15, "stores drained")]
 
 
 def build():

@@ -215,6 +215,8 @@ Layout make_layout(std::vector<TPlan>& ps) {
     for (auto& p : ps)
         if (!p.dwt) rwg += (p.pop + RES_CHUNK - 1) / RES_CHUNK;
     ce = std::max(ce, (size_t)std::min<int64_t>(rwg, RES_MAX_WG) * RES_WG_WORDS);
+    /* the one-launch small path keeps one slot of SM_SLOT_WORDS per workgroup there */
+    ce = std::max(ce, (size_t)RES_MAX_WG * SM_SLOT_WORDS);
     off = align_up(off + ce * sizeof(uint32_t));
     L.P = off;
     for (auto& p : ps) {
@@ -357,7 +359,7 @@ void inverse_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s)
 
 /* ---- the one-launch small path (small.hip) ---- */
 constexpr int64_t SM_POP_MAX = 1 << 20; /* population of a whole call taken by k_small */
-constexpr int SM_TILES_MAX = 64;        /* workgroups per tensor */
+constexpr int SM_TILES_MAX = SM_SEG_WG_MAX; /* workgroups per tensor */
 
 /* Tile sizes (TR x TC at level L) for one tensor: every tile's forward and inverse arena must
  * fit; among those, the least per-workgroup level-0 window plus a charge per workgroup. */
@@ -405,7 +407,7 @@ bool small_tiling(const TPlan& p, int F, int budget, int words, SmallSeg& sg) {
 /* k_small takes the whole call when every tensor is a 2-D transform, the call is small and
  * every tensor finds a tiling inside the co-resident grid */
 bool plan_small(const std::vector<TPlan>& ps, const wtp_tensor* ts, int n, void* ws, double pct, const Taps& tp,
-                SmallTable& t) {
+                uint32_t* slots, SmallTable& t) {
     if (n > SM_MAX_SEG || (tp.F & 1) || tp.F < 2 || tp.F > SM_F_MAX) return false;
     const int cap = std::min(resident_capacity(), RES_MAX_WG);
     int64_t tot = 0;
@@ -424,7 +426,9 @@ bool plan_small(const std::vector<TPlan>& ps, const wtp_tensor* ts, int n, void*
             return e && atoi(e) > 0 ? atoi(e) : SM_TILES_MAX;
         }();
         /* workgroups by share of the population, at least one per image */
-        const int budget = (int)std::max<int64_t>(p.B, std::min<int64_t>(tiles_max, (int64_t)cap * p.pop / tot));
+        if (p.B > SM_SEG_WG_MAX) return false;
+        const int budget = (int)std::max<int64_t>(p.B, std::min<int64_t>(std::min(tiles_max, SM_SEG_WG_MAX),
+                                                                         (int64_t)cap * p.pop / tot));
         if (!small_tiling(p, tp.F, budget, (SM_WIN_WORDS - words) / (n - i), sg)) return false;
         /* the windows of every tile row and tile column, packed (small_geom.h computes them) */
         {
@@ -475,6 +479,7 @@ bool plan_small(const std::vector<TPlan>& ps, const wtp_tensor* ts, int n, void*
     for (int i = n; i < SM_MAX_SEG; ++i) t.wg_begin[i] = INT32_MAX;
     if (wg > cap) return false;
     t.nseg = n;
+    t.slots = slots;
     t.nblk = wg;
     t.tp.F = tp.F;
     for (int i = 0; i < 4; ++i)
@@ -597,7 +602,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     if (!no_resident && !flat && g_resident.load(std::memory_order_relaxed)) {
         /* a small call: the whole path in one launch (small.hip) */
         SmallTable st;
-        if (plan_small(ps, tensors, ntensors, ws, pct, tp, st)) {
+        if (plan_small(ps, tensors, ntensors, ws, pct, tp, cand, st)) {
             for (int i = 1; i <= 4; ++i) stage(i, s);
             launch_small(st, head, results, s);
             stage(5, s);

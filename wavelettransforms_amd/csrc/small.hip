@@ -49,16 +49,21 @@ constexpr int SM_THREADS = WTP_SM_THREADS;
 static_assert(SM_THREADS >= 256 && SM_THREADS <= 1024 && (SM_THREADS & (SM_THREADS - 1)) == 0, "k_small block");
 constexpr int SM_NW = SM_THREADS / 64;
 constexpr int SM_PF = 8; /* inverse-window words per thread prefetched in registers */
+/* after the first barrier every workgroup publishes the keys of the rank's 12-bit bin in a slot
+ * of its own: [0] count (bit 31: more than fit), [1] padding zeros it counts, [2] its smallest key
+ * above the bin, then up to SM_SLOT_KEYS keys */
+constexpr int SM_SLOT_KEYS = SM_SLOT_WORDS - 3;
+constexpr int SM_GATHER = SM_SEG_WG_MAX * SM_SLOT_WORDS; /* LDS words of the gathered slots (arena tail) */
 
 /* per-segment selection state in the parity region (zero at the start of the launch) */
 struct alignas(128) SmallState {
     uint32_t bar[4][32];   /* segment barrier counters, one 128-byte line each */
     uint32_t maxkey;       /* atomicMax of every key                           */
-    uint32_t notmin;       /* atomicMax of ~key over the keys above the rank's group */
+    uint32_t notmin;       /* fallback: atomicMax of ~key over the keys above the rank's group */
     uint32_t pad[30];
-    uint32_t h1[1024];     /* key bits 30..21                                  */
-    uint32_t h2[1024];     /* bits 20..11 of the keys in the rank's h1 bin      */
-    uint32_t h3[2048];     /* bits 10..0 of the keys in the rank's 21-bit group */
+    uint32_t h1[4096];     /* key bits 30..19                                  */
+    uint32_t h2[2048];     /* fallback: bits 18..8 of the keys in the rank's h1 bin */
+    uint32_t h3[256];      /* fallback: bits 7..0 of the keys in the rank's 23-bit group */
 };
 static_assert(SM_MAX_SEG * sizeof(SmallState) <= SEG_PER_LAUNCH * sizeof(SelState), "small state fits the region");
 
@@ -120,30 +125,64 @@ __device__ __forceinline__ void sm_divmod(int e, int n, float inv, int* q, int* 
 }
 __device__ __forceinline__ int sm_wrap(int a, int N) { return a < N ? a : a - N; } /* a < 2N */
 
-/* block-wide exclusive scan of one u32 per thread; returns the exclusive prefix, *tot the sum */
+
+__device__ __forceinline__ int sm_r4(int x) { return (x + 3) & ~3; } /* LDS regions start 16-byte aligned */
+
+/* Cross-lane scan on DPP (row_shr inside rows of 16 lanes, row_bcast:15/31 across rows), as in
+ * kernels.hip: a few VALU cycles per step where a shuffle pays an LDS round trip.  Whole wave. */
+template <int CTRL, int ROWM = 0xf, int BANKM = 0xf>
+__device__ __forceinline__ uint32_t sm_dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWM, BANKM, false);
+}
+__device__ __forceinline__ uint32_t sm_wave_scan(uint32_t v) { /* inclusive */
+    v += sm_dpp<0x111>(v);
+    v += sm_dpp<0x112>(v);
+    v += sm_dpp<0x114>(v);
+    v += sm_dpp<0x118>(v);
+    v += sm_dpp<0x142, 0xa>(v);
+    v += sm_dpp<0x143, 0xc>(v);
+    return v;
+}
+
+/* wave-wide min / max / or / sum on DPP (lanes without a source keep their own value), the
+ * result read from lane 63; every lane of the wave must be active */
+template <int CTRL, int ROWM = 0xf, int BANKM = 0xf>
+__device__ __forceinline__ uint32_t sm_dppk(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROWM, BANKM, false);
+}
+template <class Op>
+__device__ __forceinline__ uint32_t sm_wave_red(uint32_t v, const Op& op) {
+    v = op(v, sm_dppk<0x111>(v));
+    v = op(v, sm_dppk<0x112>(v));
+    v = op(v, sm_dppk<0x114>(v));
+    v = op(v, sm_dppk<0x118>(v));
+    v = op(v, sm_dppk<0x142, 0xa>(v));
+    v = op(v, sm_dppk<0x143, 0xc>(v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint32_t sm_wave_min(uint32_t v) { return sm_wave_red(v, [](uint32_t a, uint32_t b) { return a < b ? a : b; }); }
+__device__ __forceinline__ uint32_t sm_wave_max(uint32_t v) { return sm_wave_red(v, [](uint32_t a, uint32_t b) { return a > b ? a : b; }); }
+__device__ __forceinline__ uint32_t sm_wave_or(uint32_t v) { return sm_wave_red(v, [](uint32_t a, uint32_t b) { return a | b; }); }
+__device__ __forceinline__ uint32_t sm_wave_sum(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)sm_wave_scan(v), 63); }
+
+/* block-wide exclusive scan of one u32 per thread (DPP inside the waves, one LDS exchange
+ * across them); *tot the block total */
 __device__ __forceinline__ uint32_t sm_scan(uint32_t v, uint32_t* wtot, uint32_t* tot) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    if (lane == 63) wtot[wv] = x;
+    const uint32_t incl = sm_wave_scan(v);
+    if (lane == 63) wtot[wv] = incl;
     __syncthreads();
     uint32_t before = 0, all = 0;
 #pragma unroll
     for (int w = 0; w < SM_NW; ++w) {
-        const uint32_t t = wtot[w];
-        before += w < wv ? t : 0u;
-        all += t;
+        const uint32_t x = wtot[w];
+        before += w < wv ? x : 0u;
+        all += x;
     }
     __syncthreads();
     *tot = all;
-    return before + x - v;
+    return before + incl - v;
 }
-
-__device__ __forceinline__ int sm_r4(int x) { return (x + 3) & ~3; } /* LDS regions start 16-byte aligned */
 
 /* Taps of one output, summed in PyWavelets' order (wt_dwt_core.h).  The interior form -- taps
  * j = 0, 1, ... ascending at consecutive descending window slots -- is recognised by its first
@@ -257,7 +296,7 @@ template <int FT>
 __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* __restrict__ head,
                                                       wtp_result* __restrict__ res) {
     __shared__ __attribute__((aligned(16))) float arena[SM_ARENA];
-    __shared__ uint32_t hist[2048];
+    __shared__ uint32_t hist[4096];
     __shared__ SmAxis axr, axc;
     __shared__ uint32_t wtot[SM_NW], wred[SM_NW];
     __shared__ int s_ok, s_dig[2];
@@ -309,7 +348,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
             sm_stc(&res[g.res].path, 0);
         }
     }
-    for (int i = tid; i < 1024; i += SM_THREADS) hist[i] = 0u;
+    for (int i = tid; i < 4096; i += SM_THREADS) hist[i] = 0u;
     __syncthreads();
     SM_PROBE(0);
 
@@ -391,7 +430,6 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
             }
         }
         __syncthreads();
-        if (k <= 3) SM_PROBE(3 * k - 1 - (k > 1));
         /* axis -1: aa, ad from the L rows, da, dd from the H rows; aa is the next level's input */
         {
             const int n = wr.len * wc.len;
@@ -444,15 +482,19 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                     K[li] = k1;
                     K[li + plane] = k2;
                     K[li + 2 * plane] = k3;
-                    atomicAdd(&hist[k1 >> 21], 1u);
-                    atomicAdd(&hist[k2 >> 21], 1u);
-                    atomicAdd(&hist[k3 >> 21], 1u);
+#ifndef WTP_SM_NOHIST /* lab only: time the histogram's LDS atomics */
+                    atomicAdd(&hist[k1 >> 19], 1u);
+                    atomicAdd(&hist[k2 >> 19], 1u);
+                    atomicAdd(&hist[k3 >> 19], 1u);
+#endif
                     mx = max(mx, max(k1, max(k2, k3)));
                     if (last) {
                         sm_stc(P + (int64_t)r * g.PC + c, aa);
                         const uint32_t k0 = sm_abs_key(aa);
                         K[li + 3 * plane] = k0;
-                        atomicAdd(&hist[k0 >> 21], 1u);
+#ifndef WTP_SM_NOHIST
+                        atomicAdd(&hist[k0 >> 19], 1u);
+#endif
                         mx = max(mx, k0);
                     }
                 }
@@ -460,15 +502,12 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
             kbase += (3 + last) * plane;
         }
         __syncthreads();
-        if (k <= 3) SM_PROBE(3 * k - (k > 1));
     }
     /* the packed array's padding (non-tight layouts) holds zeros: keys 0, counted by tile 0 */
     const uint32_t npad = lt == 0 ? (uint32_t)g.npad : 0u;
     if (tid == 0 && npad) hist[0] += npad;
     {
-        uint32_t m = mx;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+        const uint32_t m = sm_wave_max(mx);
         if (lane == 0) wred[wv] = m;
     }
     __syncthreads();
@@ -477,7 +516,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
         for (int w = 0; w < SM_NW; ++w) m = max(m, wred[w]);
         atomicMax(&st->maxkey, m);
     }
-    for (int i = tid; i < 1024; i += SM_THREADS)
+    for (int i = tid; i < 4096; i += SM_THREADS)
         if (hist[i]) atomicAdd(&st->h1[i], hist[i]);
     const uint32_t nwg = (uint32_t)g.nwg;
     const uint32_t a0 = sm_arrive(&st->bar[0][0]);
@@ -519,120 +558,235 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
         return P + (int64_t)rr * g.PC + cc;
     };
 
-    /* ---------------- S: three digits of the lower rank ---------------- */
-    const int64_t r0 = g.r0;
-    int64_t rem = r0; /* rank inside the current group */
-    uint32_t prefix = 0;
-    auto pick = [&](const uint32_t* gh, int nb, int shift) { /* the digit holding rank `rem` */
-        const int per = nb / SM_THREADS;
-        uint32_t c[2048 / SM_THREADS], cs = 0;
+    /* ---------------- S: the two order statistics ---------------- */
+    /* locate ranks ra <= rb in nb bins (get(i): count of bin i, every load of a thread issued
+     * before the first is used): s_dig[x] = the bin holding rank x (-1: past the total),
+     * s_bef[x] = keys in the bins before it */
+    auto locate = [&](auto get, int nb, int64_t ra, int64_t rb) {
+        constexpr int MAXP = 4096 / SM_THREADS;
+        const int per = nb >= SM_THREADS ? nb / SM_THREADS : 1;
+        uint32_t c[MAXP], cs = 0;
 #pragma unroll
-        for (int u = 0; u < 2048 / SM_THREADS; ++u) c[u] = u < per ? sm_ldc(gh + tid * per + u) : 0u;
+        for (int u = 0; u < MAXP; ++u) {
+            const int i = tid * per + u;
+            c[u] = (u < per && i < nb) ? get(i) : 0u;
+        }
 #pragma unroll
-        for (int u = 0; u < 2048 / SM_THREADS; ++u) cs += c[u];
+        for (int u = 0; u < MAXP; ++u) cs += c[u];
+        if (tid < 2) s_dig[tid] = -1;
         uint32_t tot;
         const uint32_t ex = sm_scan(cs, wtot, &tot);
         uint32_t e = ex;
-        for (int u = 0; u < per; ++u) {
-            if (rem >= (int64_t)e && rem < (int64_t)(e + c[u])) { s_dig[0] = tid * per + u; s_bef[0] = e; }
+#pragma unroll
+        for (int u = 0; u < MAXP; ++u) {
+            if (ra >= (int64_t)e && ra < (int64_t)(e + c[u])) { s_dig[0] = tid * per + u; s_bef[0] = e; }
+            if (rb >= (int64_t)e && rb < (int64_t)(e + c[u])) { s_dig[1] = tid * per + u; s_bef[1] = e; }
             e += c[u];
         }
         __syncthreads();
-        rem -= s_bef[0];
-        prefix = (prefix << (shift)) | (uint32_t)s_dig[0];
-        return tot;
     };
+    const int64_t ra0 = g.r0, rb0 = g.above ? g.r0 : g.r0 + 1;
+    uint32_t ka = 0, kb = 0, mk = 0;
+    int64_t rem = 0; /* ra inside the rank's 12-bit bin */
+    uint32_t d1 = 0, cnt1 = 0;
+    __shared__ uint32_t s_fill, s_min[2];
+    bool ovf = false;
+    uint32_t* G = reinterpret_cast<uint32_t*>(arena + SM_ARENA - SM_GATHER);
     if (ok) {
-        pick(st->h1, 1024, 0);
-        /* pass 2: bits 20..11 of the keys in the rank's bin */
-        for (int i = tid; i < 1024; i += SM_THREADS) hist[i] = 0u;
-        __syncthreads();
-        const uint32_t p1 = prefix;
-        for (int i = tid; i < nkeys; i += SM_THREADS) {
-            const uint32_t k = K[i];
-            if ((k >> 21) == p1) atomicAdd(&hist[(k >> 11) & 1023u], 1u);
-        }
-        if (tid == 0 && npad && p1 == 0) hist[0] += npad;
-        __syncthreads();
-        for (int i = tid; i < 1024; i += SM_THREADS)
-            if (hist[i]) atomicAdd(&st->h2[i], hist[i]);
-        const uint32_t a1 = sm_arrive(&st->bar[1][0]);
-        /* every level's coefficient windows of the inverse, from P (complete since barrier 0):
-         * issued now, their round trip hidden behind this barrier's wait */
-        float pv[SM_PF];
-#pragma unroll
-        for (int u = 0; u < SM_PF; ++u) {
-            const int e = tid + u * SM_THREADS;
-            pv[u] = e < nwin ? sm_ldc(win_src(e)) : 0.0f;
-        }
-        ok = sm_wait(&st->bar[1][0], a1, nwg, tmo, &s_ok);
-#pragma unroll
-        for (int u = 0; u < SM_PF; ++u) {
-            const int e = tid + u * SM_THREADS;
-            if (e < nwin) WIN[e] = pv[u];
-        }
-        for (int e = tid + SM_PF * SM_THREADS; e < nwin; e += SM_THREADS) WIN[e] = sm_ldc(win_src(e));
-        SM_PROBE(12);
-    }
-    if (ok) {
-        pick(st->h2, 1024, 10);
-        /* pass 3: bits 10..0 of the keys in the rank's 21-bit group, and the smallest key above it */
-        for (int i = tid; i < 2048; i += SM_THREADS) hist[i] = 0u;
-        __syncthreads();
-        const uint32_t p2 = prefix;
+        /* digit 1: the 12-bit bin of ra */
+        if (tid == 0) { s_fill = 0; s_min[0] = 0xFFFFFFFFu; s_min[1] = 0xFFFFFFFFu; }
+        locate([&](int i) { return sm_ldc(st->h1 + i); }, 4096, ra0, ra0);
+        d1 = (uint32_t)s_dig[0];
+        rem = ra0 - s_bef[0];
+        SM_PROBE(2);
+        /* this workgroup's keys of that bin into its slot, its smallest key above the bin */
+        uint32_t* slot = t.slots + (int64_t)blockIdx.x * SM_SLOT_WORDS;
         uint32_t mn = 0xFFFFFFFFu;
         for (int i = tid; i < nkeys; i += SM_THREADS) {
             const uint32_t k = K[i];
-            const uint32_t g21 = k >> 11;
-            if (g21 == p2) atomicAdd(&hist[k & 2047u], 1u);
-            else if (g21 > p2) mn = min(mn, k);
+            const uint32_t b12 = k >> 19;
+            if (b12 == d1) {
+                const uint32_t p = atomicAdd(&s_fill, 1u);
+                if (p < (uint32_t)SM_SLOT_KEYS) sm_stc(slot + 3 + p, k);
+            } else if (b12 > d1) {
+                mn = min(mn, k);
+            }
         }
-        if (tid == 0 && npad && p2 == 0) hist[0] += npad;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, d, 64));
-        if (lane == 0) wred[wv] = mn;
+        mn = sm_wave_min(mn);
+        if (lane == 0 && mn != 0xFFFFFFFFu) atomicMin(&s_min[0], mn);
         __syncthreads();
         if (tid == 0) {
-            uint32_t m = 0xFFFFFFFFu;
-            for (int w = 0; w < SM_NW; ++w) m = min(m, wred[w]);
-            if (m != 0xFFFFFFFFu) atomicMax(&st->notmin, ~m);
+            const uint32_t f = s_fill;
+            sm_stc(slot, min(f, (uint32_t)SM_SLOT_KEYS) | (f > (uint32_t)SM_SLOT_KEYS ? 0x80000000u : 0u));
+            sm_stc(slot + 1, (npad && d1 == 0) ? npad : 0u);
+            sm_stc(slot + 2, s_min[0]);
         }
+        SM_PROBE(3);
+        const uint32_t a1 = sm_arrive(&st->bar[1][0]);
+        SM_PROBE(4);
+        /* every level's coefficient windows of the inverse, from P (complete since barrier 0):
+         * issued now, their round trip hidden behind this barrier's wait */
+#ifdef WTP_SM_PF0 /* lab: wave 0 (the polling wave) issues none of the prefetch */
+        constexpr int PB = 64;
+#else
+        constexpr int PB = 0;
+#endif
+        constexpr int PT = SM_THREADS - PB;
+        float pv[SM_PF];
+#pragma unroll
+        for (int u = 0; u < SM_PF; ++u) {
+            const int e = tid - PB + u * PT;
+            pv[u] = (tid >= PB && e < nwin) ? sm_ldc(win_src(e)) : 0.0f;
+        }
+        ok = sm_wait(&st->bar[1][0], a1, nwg, tmo, &s_ok);
+        SM_PROBE(5);
+#pragma unroll
+        for (int u = 0; u < SM_PF; ++u) {
+            const int e = tid - PB + u * PT;
+            if (tid >= PB && e < nwin) WIN[e] = pv[u];
+        }
+        for (int e = tid + SM_PF * PT; e < nwin; e += SM_THREADS) WIN[e] = sm_ldc(win_src(e));
+        SM_PROBE(7);
+    }
+    if (ok) {
+        /* every slot of the segment into LDS (and the segment's largest key, final since barrier 0) */
+        mk = sm_ldc(&st->maxkey);
+        const uint32_t* segs = t.slots + (int64_t)g.wg_begin * SM_SLOT_WORDS;
+        const int nw = (int)nwg * SM_SLOT_WORDS;
+        constexpr int GPT = SM_GATHER / SM_THREADS;
+        uint32_t gv[GPT];
+#pragma unroll
+        for (int u = 0; u < GPT; ++u) {
+            const int i = tid + u * SM_THREADS;
+            gv[u] = i < nw ? sm_ldc(segs + i) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < GPT; ++u) {
+            const int i = tid + u * SM_THREADS;
+            if (i < nw) G[i] = gv[u];
+        }
+        for (int i = tid; i < 1536; i += SM_THREADS) hist[i] = 0u; /* pass A bins, then pass B's */
+        if (tid == 0) s_min[1] = 0xFFFFFFFFu;
+        __syncthreads();
+        SM_PROBE(8);
+        /* the slot headers (nwg <= 64: wave 0 reduces them) */
+        __shared__ uint32_t s_hdr[4];
+        if (wv == 0) {
+            uint32_t c0 = 0, zz = 0, mw = 0xFFFFFFFFu;
+            if (lane < (int)nwg) {
+                c0 = G[lane * SM_SLOT_WORDS];
+                zz = G[lane * SM_SLOT_WORDS + 1];
+                mw = G[lane * SM_SLOT_WORDS + 2];
+            }
+            const uint32_t o = sm_wave_or(c0 & 0x80000000u), c = sm_wave_sum(c0 & 0x7FFFFFFFu);
+            zz = sm_wave_sum(zz);
+            mw = sm_wave_min(mw);
+            if (lane == 0) { s_hdr[0] = o; s_hdr[1] = c; s_hdr[2] = zz; s_hdr[3] = mw; }
+        }
+        /* a thread's keys: entries tid + u * SM_THREADS of the slot array, read while wave 0 reduces */
+        constexpr int KPT = SM_SEG_WG_MAX * SM_SLOT_KEYS / SM_THREADS + 1;
+        uint32_t kk[KPT];
+        bool kv[KPT];
+#pragma unroll
+        for (int u = 0; u < KPT; ++u) {
+            const int i = tid + u * SM_THREADS;
+            const int w = i / SM_SLOT_KEYS, j = i - w * SM_SLOT_KEYS;
+            const bool in = w < (int)nwg;
+            const uint32_t c = in ? G[w * SM_SLOT_WORDS] & 0x7FFFFFFFu : 0u;
+            kk[u] = in ? G[w * SM_SLOT_WORDS + 3 + j] : 0u;
+            kv[u] = j < (int)c;
+        }
+        __syncthreads();
+        const uint32_t z = s_hdr[2], mnab = s_hdr[3];
+        cnt1 = s_hdr[1] + z;
+        ovf = s_hdr[0] != 0;
+        SM_PROBE(9);
+        if (!ovf) {
+            /* the exact ranks among the gathered keys: bits 18..9, then 8..0 (the padding zeros
+             * carry zero digits) */
+            const int64_t rbi = rb0 - (ra0 - rem); /* rb inside the bin */
+#pragma unroll
+            for (int u = 0; u < KPT; ++u)
+                if (kv[u]) atomicAdd(&hist[(kk[u] >> 9) & 1023u], 1u);
+            if (tid == 0 && z) hist[0] += z;
+            __syncthreads();
+            locate([&](int i) { return hist[i]; }, 1024, rem, min(rbi, (int64_t)cnt1 - 1));
+            const uint32_t da = (uint32_t)s_dig[0], db = (uint32_t)s_dig[1];
+            const int64_t ra2 = rem - s_bef[0], rb2 = rbi - s_bef[0];
+            SM_PROBE(12);
+            uint32_t* hb = hist + 1024;
+            uint32_t mnA = 0xFFFFFFFFu;
+#pragma unroll
+            for (int u = 0; u < KPT; ++u) {
+                const uint32_t a = (kk[u] >> 9) & 1023u;
+                if (kv[u] && a == da) atomicAdd(&hb[kk[u] & 511u], 1u);
+                else if (kv[u] && a > da) mnA = min(mnA, kk[u]);
+            }
+            mnA = sm_wave_min(mnA);
+            if (lane == 0 && mnA != 0xFFFFFFFFu) atomicMin(&s_min[1], mnA);
+            if (tid == 0 && z && da == 0) hb[0] += z;
+            __syncthreads();
+            locate([&](int i) { return hb[i]; }, 512, ra2, rb2);
+            ka = (d1 << 19) | (da << 9) | (uint32_t)s_dig[0];
+            if (rbi >= (int64_t)cnt1) kb = mnab;             /* rb past the bin: the next key above it */
+            else if (db != da) kb = s_min[1];                /* rb in a later 10-bit group of the bin */
+            else kb = (d1 << 19) | (da << 9) | (uint32_t)s_dig[1];
+        }
+        SM_PROBE(13);
+    }
+    if (ok && ovf) {
+        /* fallback (a workgroup held more keys of the bin than its slot): two more digits over the
+         * segment, bits 18..8 and 7..0, each through the segment's histograms and a barrier */
+        int64_t r = rem;
+        uint32_t prefix = d1;
+        __syncthreads();
+        for (int i = tid; i < 2048; i += SM_THREADS) hist[i] = 0u;
+        __syncthreads();
+        for (int i = tid; i < nkeys; i += SM_THREADS) {
+            const uint32_t k = K[i];
+            if ((k >> 19) == prefix) atomicAdd(&hist[(k >> 8) & 2047u], 1u);
+        }
+        if (tid == 0 && npad && prefix == 0) hist[0] += npad;
+        __syncthreads();
         for (int i = tid; i < 2048; i += SM_THREADS)
-            if (hist[i]) atomicAdd(&st->h3[i], hist[i]);
+            if (hist[i]) atomicAdd(&st->h2[i], hist[i]);
         const uint32_t a2 = sm_arrive(&st->bar[2][0]);
         ok = sm_wait(&st->bar[2][0], a2, nwg, tmo, &s_ok);
-        SM_PROBE(13);
+        if (ok) {
+            locate([&](int i) { return sm_ldc(st->h2 + i); }, 2048, r, r);
+            r -= s_bef[0];
+            prefix = (prefix << 11) | (uint32_t)s_dig[0];
+            for (int i = tid; i < 256; i += SM_THREADS) hist[i] = 0u;
+            if (tid == 0) s_min[0] = 0xFFFFFFFFu;
+            __syncthreads();
+            uint32_t mn = 0xFFFFFFFFu;
+            for (int i = tid; i < nkeys; i += SM_THREADS) {
+                const uint32_t k = K[i];
+                if ((k >> 8) == prefix) atomicAdd(&hist[k & 255u], 1u);
+                else if ((k >> 8) > prefix) mn = min(mn, k);
+            }
+            mn = sm_wave_min(mn);
+            if (lane == 0 && mn != 0xFFFFFFFFu) atomicMin(&s_min[0], mn);
+            if (tid == 0 && npad && prefix == 0) hist[0] += npad;
+            __syncthreads();
+            if (tid == 0 && s_min[0] != 0xFFFFFFFFu) atomicMax(&st->notmin, ~s_min[0]);
+            for (int i = tid; i < 256; i += SM_THREADS)
+                if (hist[i]) atomicAdd(&st->h3[i], hist[i]);
+            const uint32_t a3 = sm_arrive(&st->bar[3][0]);
+            ok = sm_wait(&st->bar[3][0], a3, nwg, tmo, &s_ok);
+        }
+        if (ok) {
+            const int64_t rb = g.above ? r : r + 1;
+            locate([&](int i) { return sm_ldc(st->h3 + i); }, 256, r, rb);
+            ka = (prefix << 8) | (uint32_t)s_dig[0];
+            kb = s_dig[1] >= 0 ? ((prefix << 8) | (uint32_t)s_dig[1]) : ~sm_ldc(&st->notmin);
+        }
     }
     if (!ok) {
         if (tid == 0) atomicMax(&res[g.res].path, (int32_t)MODE_FAULT);
         return; /* nothing stored to `out`: the caller's input and output are untouched */
     }
-    /* the last digit: both ranks from one histogram, r0 + 1 past the group -> the smallest key above */
-    uint32_t ka, kb;
-    {
-        constexpr int PER = 2048 / SM_THREADS;
-        const uint32_t* gh = st->h3;
-        uint32_t c[PER], cs = 0;
-#pragma unroll
-        for (int u = 0; u < PER; ++u) c[u] = sm_ldc(gh + PER * tid + u);
-#pragma unroll
-        for (int u = 0; u < PER; ++u) cs += c[u];
-        if (tid < 2) { s_dig[tid] = -1; }
-        uint32_t tot;
-        const uint32_t ex = sm_scan(cs, wtot, &tot);
-        const int64_t ra = rem, rb = g.above ? rem : rem + 1;
-        uint32_t e = ex;
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            if (ra >= (int64_t)e && ra < (int64_t)(e + c[u])) s_dig[0] = PER * tid + u;
-            if (rb >= (int64_t)e && rb < (int64_t)(e + c[u])) s_dig[1] = PER * tid + u;
-            e += c[u];
-        }
-        __syncthreads();
-        ka = (prefix << 11) | (uint32_t)s_dig[0];
-        kb = s_dig[1] >= 0 ? ((prefix << 11) | (uint32_t)s_dig[1]) : ~sm_ldc(&st->notmin);
-    }
-    const uint32_t mk = sm_ldc(&st->maxkey);
+    if (ovf) mk = sm_ldc(&st->maxkey);
     /* threshold: numpy/lib/function_base.py _lerp -- diff in float32, the blend in float64 */
     const float fa = __uint_as_float(ka), fb = __uint_as_float(kb);
     const float diff = fb - fa;
@@ -643,6 +797,10 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     auto tl = [&](float c) { return (fabsf(c) < thr32) ? 0.0f : c; };
 
     /* ---------------- I: synthesis of the owned output block ---------------- */
+#ifdef WTP_SM_NOPF
+    for (int e = tid; e < nwin; e += SM_THREADS) WIN[e] = sm_ldc(win_src(e));
+    __syncthreads();
+#endif
     for (int e = tid; e < nwin; e += SM_THREADS) WIN[e] = tl(WIN[e]); /* the np.where of :31 */
     __syncthreads();
     int ia = 0, ilh = 0;
@@ -762,10 +920,8 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
         __syncthreads();
     }
     {
-        unsigned long long zz = z;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) zz += __shfl_xor(zz, d, 64);
-        if (lane == 0) wred[wv] = (uint32_t)zz;
+        const uint32_t zz = sm_wave_sum((uint32_t)z);
+        if (lane == 0) wred[wv] = zz;
         __syncthreads();
         if (tid == 0) {
             unsigned long long s = 0;

@@ -209,7 +209,9 @@ void launch_resident(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_res
 /* ---- the small-population path in one launch (small.hip, k_small) ----
  * every tensor of the call is a 2-D transform whose tiles fit one workgroup's LDS; one
  * workgroup per tile, the tiles of a tensor are its segment (small_geom.h) */
-constexpr int SM_MAX_SEG = 6;       /* tensors per call */
+constexpr int SM_MAX_SEG = 4;       /* tensors per call */
+constexpr int SM_SEG_WG_MAX = 64;   /* workgroups per tensor */
+constexpr int SM_SLOT_WORDS = 128;  /* per workgroup in the candidate region: the keys of the rank's bin */
 constexpr int SM_ARENA = 34 * 1024; /* LDS words of a workgroup's arena (136 KB) */
 constexpr int SM_F_MAX = 20;        /* longest filter */
 constexpr int SM_LMAX = 10;         /* = SM_MAX_L of small_geom.h */
@@ -240,6 +242,7 @@ struct SmallTable {
     uint32_t timeout; /* set by launch_small */
     int32_t pad;
     unsigned long long* stamps;
+    uint32_t* slots;              /* SM_SLOT_WORDS per workgroup (the workspace's candidate region) */
     int32_t wg_begin[SM_MAX_SEG]; /* INT32_MAX past nseg */
     SmallSeg s[SM_MAX_SEG];
     SmallTaps tp;
