@@ -277,6 +277,8 @@ def main():
     resident = (not args.no_resident and not args.flatten and recs and all(r["eff_level"] == 0 for r in recs)
                 and len(xs) <= 24 and sum(-(-x.numel() // 49152) for x in xs) <= engine.resident_capacity())
     has_dwt = any(r["eff_level"] > 0 for r in recs)
+    # the whole call as one k_small launch (csrc/small.hip): small 2-D calls, e.g. cfg3
+    small = bool(recs) and not sharded and all(r["path"] == engine.MODE_SMALL for r in recs)
 
     # ------------------------------------------------- hipGraph (single-process configs)
     G = max(1, min(args.graph_steps, args.steps))
@@ -363,12 +365,14 @@ def main():
         return (h[:, 1] - h[:, 0]).astype(np.float64) * 0.01  # 100 MHz ticks -> us
 
     stage_us, dom, dom_us, dom_bytes, dom_launches, timing_src = {}, None, None, 0, 1, None
-    if resident and xs:
+    if (resident or small) and xs:
+        # one launch per step: its algorithmic bytes are every weight read once and written once
         spans = stamp_spans(args.stamp_reps)
-        dom, dom_us, dom_bytes = "k_resident", float(np.mean(spans)), 8 * n_w
+        dom = "k_resident" if resident else "k_small"
+        dom_us, dom_bytes = float(np.mean(spans)), 8 * n_w
         timing_src = ("in-kernel s_memrealtime stamps: first workgroup start -> last workgroup end after its "
                       "stores completed, mean of %d back-to-back launches (wtp_set_kernel_stamps)" % len(spans))
-        stage_us = {"k_resident": dom_us}
+        stage_us = {dom: dom_us}
     elif xs:
         # stage intervals from HIP events the library records between its launches (include dispatch
         # gaps); a spin kernel in front lets the whole call be enqueued before it runs
@@ -401,12 +405,12 @@ def main():
         dom_launches = max(r["eff_level"] for r in recs) if dom in DWT_STAGES else 1
         timing_src = ("HIP events around the stage on the library's stream (median of %d calls; the interval "
                       "includes dispatch gaps)" % args.stage_reps)
-    dom_kernel = dom if dom == "k_resident" else KERNEL_OF_STAGE.get(dom, dom)
+    dom_kernel = dom if dom in ("k_resident", "k_small") else KERNEL_OF_STAGE.get(dom, dom)
     if dom_us is not None and dom_us > ms_per_step * 1e3 and world == 1:
         timing_src += "; capped at ms_per_step"
         dom_us = ms_per_step * 1e3
     traffic, traffic_src, traffic_tag = pmc_traffic(args.config, dom_kernel) if dom else (None, None, None)
-    stamps_us = dom_us if dom == "k_resident" else None
+    stamps_us = dom_us if dom in ("k_resident", "k_small") else None
     prof_ns, prof_calls = rocprof_kernel(prof_stats, dom_kernel) if dom else (0.0, 0)
     if prof_calls:
         # the durations rocprofv3 records for the dominant kernel in the child run of this
@@ -436,10 +440,10 @@ def main():
                 "ms_per_step_p90": float(np.percentile(cms, 90)), "reps": len(cev),
                 "note": "a 512 MiB write between steps evicts the 256 MiB Infinity Cache; eager launches, "
                         "per-step HIP events (include the launch's dispatch gap)"}
-        if resident:
+        if resident or small:
             cspans = stamp_spans(args.cold_reps, before=lambda: flush.fill_(1.0))
             cus = float(np.mean(cspans))
-            cold["k_resident_us"] = cus
+            cold[dom + "_us"] = cus
             cold["roofline_frac"] = dom_bytes / (cus * 1e-6) / 1e9 / HBM_PEAK_GBS
         del flush
 

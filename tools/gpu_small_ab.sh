@@ -23,3 +23,10 @@ if [ -n "$SM_TILES_SWEEP" ]; then
     grep -E "workgroups|arrived|digit 3|stores" "$OUT/probe_t$n.log"
   done
 fi
+if [ -n "$SM_COST_SWEEP" ]; then
+  for c in $SM_COST_SWEEP; do
+    echo "== tile cost $c"
+    WTP_SM_TILES=128 WTP_SM_TILECOST=$c PROBE_OUT=$ROOT/tools/mb/libwtprune_probe.so timeout -k 10 120 python -u tools/probe_small.py > "$OUT/probe_c$c.log" 2>&1 || { echo "probe failed"; exit 1; }
+    grep -E "workgroups|L0 loaded|arrived 0|barrier|ranks|I start|stores" "$OUT/probe_c$c.log"
+  done
+fi

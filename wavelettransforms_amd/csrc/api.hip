@@ -377,7 +377,7 @@ bool small_tiling(const TPlan& p, int F, int budget, int words, SmallSeg& sg) {
         for (int TC = CL;; TC = (TC + 1) / 2) {
             const int tC = (CL + TC - 1) / TC;
             const int64_t tiles = p.B * tR * tC;
-            if (tiles <= budget && 3 * (L + 1) * (tR + tC) <= words) {
+            if (tiles <= budget && 2 * (L + 1) * (tR + tC) <= words) {
                 ac.resize(tC);
                 for (int j = 0; j < tC; ++j) sm_axis(j, TC, L, Cn, F, &ac[j]);
                 int64_t worst = 0;
@@ -388,7 +388,11 @@ bool small_tiling(const TPlan& p, int F, int budget, int words, SmallSeg& sg) {
                         fits = sm_fwd_words(nd) <= SM_ARENA && sm_inv_words(nd) <= SM_ARENA;
                         worst = std::max<int64_t>(worst, (int64_t)ar[i].fw[0].len * ac[j].fw[0].len + nd.fkeys / 2);
                     }
-                const int64_t cost = worst + 64 * tiles;
+                static const int64_t tile_cost = [] { /* lab knob: LDS words a workgroup is worth */
+                    const char* e = getenv("WTP_SM_TILECOST");
+                    return e && atoi(e) >= 0 ? (int64_t)atoi(e) : (int64_t)64;
+                }();
+                const int64_t cost = worst + tile_cost * tiles;
                 if (fits && cost < best) {
                     best = cost;
                     sg.TR = TR;
@@ -439,7 +443,6 @@ bool plan_small(const std::vector<TPlan>& ps, const wtp_tensor* ts, int n, void*
                 for (int k = 0; k <= p.L; ++k) {
                     t.win[words++] = (uint32_t)a.fw[k].s | ((uint32_t)a.fw[k].len << 16);
                     t.win[words++] = (uint32_t)a.sv[k].s | ((uint32_t)a.sv[k].len << 16);
-                    t.win[words++] = (uint32_t)a.olo[k] | ((uint32_t)a.ohi[k] << 16);
                 }
             };
             SmAxis a;

@@ -54,6 +54,7 @@ constexpr int SM_PF = 8; /* inverse-window words per thread prefetched in regist
  * above the bin, then up to SM_SLOT_KEYS keys */
 constexpr int SM_SLOT_KEYS = SM_SLOT_WORDS - 3;
 constexpr int SM_GATHER = SM_SEG_WG_MAX * SM_SLOT_WORDS; /* LDS words of the gathered slots (arena tail) */
+static_assert(SM_GATHER == 8192, "small_geom.h's sm_inv_words reserves 8192 words for the gathered slots");
 
 /* per-segment selection state in the parity region (zero at the start of the launch) */
 struct alignas(128) SmallState {
@@ -328,18 +329,22 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     const uint64_t tmo = t.timeout;
     /* the tile's windows (computed by the host, small_geom.h) and the taps: one word per lane */
     {
-        const int lw = 3 * (L + 1);
+        const int lw = 2 * (L + 1);
         const uint32_t* rw = t.win + g.win_off + tr * lw;
         const uint32_t* cw = t.win + g.win_off + g.tilesR * lw + tc * lw;
         if (tid < 2 * lw) {
             const bool cols = tid >= lw;
-            const int x = cols ? tid - lw : tid, k = x / 3, f = x - 3 * k;
+            const int x = cols ? tid - lw : tid, k = x >> 1;
             const uint32_t w = cols ? cw[x] : rw[x];
             SmAxis& ax = cols ? axc : axr;
             const int lo = (int)(w & 0xFFFFu), hi = (int)(w >> 16);
-            if (f == 0) ax.fw[k] = SmIvl{lo, hi};
-            else if (f == 1) ax.sv[k] = SmIvl{lo, hi};
-            else { ax.olo[k] = lo; ax.ohi[k] = hi; }
+            if (x & 1) ax.sv[k] = SmIvl{lo, hi};
+            else ax.fw[k] = SmIvl{lo, hi};
+        } else if (tid >= 64 && tid < 64 + 2 * (L + 1)) { /* the owned ranges: shifts of the tile index */
+            const bool cols = tid >= 64 + L + 1;
+            const int k = tid - 64 - (cols ? L + 1 : 0);
+            SmAxis& ax = cols ? axc : axr;
+            sm_own(cols ? tc : tr, cols ? g.TC : g.TR, L, k, cols ? g.C : g.R, &ax.olo[k], &ax.ohi[k]);
         } else if (tid >= 128 && tid < 128 + 4 * SM_F_MAX) {
             const int i = (tid - 128) / SM_F_MAX, j = (tid - 128) - i * SM_F_MAX;
             staps[i][j] = t.tp.f[i][j];
@@ -394,6 +399,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     __syncthreads();
     SM_PROBE(1);
     int kbase = 0;
+    float* Xc = X;
     for (int k = 1; k <= L; ++k) {
         const SmIvl wr = axr.fw[k], wc = axc.fw[k], pr = axr.fw[k - 1], pc = axc.fw[k - 1];
         const int Nr = g.R[k], Nc = g.C[k], Npr = g.R[k - 1], Npc = g.C[k - 1];
@@ -410,7 +416,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                     const int s0 = fb >> 5, c1 = fb & 31;
                     float v[FT > 0 ? FT : 1];
 #pragma unroll
-                    for (int qq = 0; qq < FT; ++qq) v[qq] = X[(s0 - qq) * pc.len + mc];
+                    for (int qq = 0; qq < FT; ++qq) v[qq] = Xc[(s0 - qq) * pc.len + mc];
                     sm_order<FT>(c1, __all(c1 == 0), [&](int j) { return v[j]; }, [&](int j) { return j; },
                                  [&](int j, float x) {
                                      a = a + staps[0][j] * x;
@@ -421,15 +427,15 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                     for (int qq = 0; qq < F; ++qq) {
                         int j;
                         const int sl = sm_ana_tap(an, pr, Npr, qq, &j);
-                        const float v = X[sl * pc.len + mc];
+                        const float v = Xc[sl * pc.len + mc];
                         a = a + staps[0][j] * v;
                         d = d + staps[1][j] * v;
                     }
                 }
                 LH[e] = make_float2(a, d);
             }
+            __syncthreads();
         }
-        __syncthreads();
         /* axis -1: aa, ad from the L rows, da, dd from the H rows; aa is the next level's input */
         {
             const int n = wr.len * wc.len;
@@ -469,7 +475,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                         dd = dd + c1 * v.y;
                     }
                 }
-                if (!last) X[e] = aa;
+                if (!last) Xc[e] = aa;
                 const int r = sm_wrap(wr.s + mr, Nr), c = sm_wrap(wc.s + mc, Nc);
                 const int lr = r - axr.olo[k], lc = c - axc.olo[k];
                 if (lr >= 0 && lr < ohr && lc >= 0 && lc < ohc) {
@@ -669,16 +675,18 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
         if (tid == 0) s_min[1] = 0xFFFFFFFFu;
         __syncthreads();
         SM_PROBE(8);
-        /* the slot headers (nwg <= 64: wave 0 reduces them) */
+        /* the slot headers (wave 0 reduces them) */
         __shared__ uint32_t s_hdr[4];
         if (wv == 0) {
-            uint32_t c0 = 0, zz = 0, mw = 0xFFFFFFFFu;
-            if (lane < (int)nwg) {
-                c0 = G[lane * SM_SLOT_WORDS];
-                zz = G[lane * SM_SLOT_WORDS + 1];
-                mw = G[lane * SM_SLOT_WORDS + 2];
+            uint32_t oo = 0, cc = 0, zz = 0, mw = 0xFFFFFFFFu;
+            for (int w = lane; w < (int)nwg; w += 64) {
+                const uint32_t c0 = G[w * SM_SLOT_WORDS];
+                oo |= c0 & 0x80000000u;
+                cc += c0 & 0x7FFFFFFFu;
+                zz += G[w * SM_SLOT_WORDS + 1];
+                mw = min(mw, G[w * SM_SLOT_WORDS + 2]);
             }
-            const uint32_t o = sm_wave_or(c0 & 0x80000000u), c = sm_wave_sum(c0 & 0x7FFFFFFFu);
+            const uint32_t o = sm_wave_or(oo), c = sm_wave_sum(cc);
             zz = sm_wave_sum(zz);
             mw = sm_wave_min(mw);
             if (lane == 0) { s_hdr[0] = o; s_hdr[1] = c; s_hdr[2] = zz; s_hdr[3] = mw; }
@@ -801,8 +809,8 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     for (int e = tid; e < nwin; e += SM_THREADS) WIN[e] = sm_ldc(win_src(e));
     __syncthreads();
 #endif
-    for (int e = tid; e < nwin; e += SM_THREADS) WIN[e] = tl(WIN[e]); /* the np.where of :31 */
-    __syncthreads();
+    /* the np.where of :31 is applied as the packed coefficients are read below (tA: the cA plane
+     * of level L, packed too; the synthesised ones are not thresholded) */
     int ia = 0, ilh = 0;
     for (int k = 1; k <= L; ++k) {
         ia = max(ia, axr.sv[k].len * axc.sv[k].len);
@@ -822,6 +830,8 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
         const float* cH = cV + ns;
         const float* cD = cH + ns;
         const float* cA = k == L ? cD + ns : A;
+        const bool topA = k == L;
+        auto tA = [&](float c) { return topA ? tl(c) : c; };
         constexpr int HT = FT / 2;
         if (k == L) SM_PROBE(14);
         /* axis -1: lo = rec(cA, cV), hi = rec(cH, cD) at every source row, output columns oc */
@@ -840,10 +850,10 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                     float va[HT > 0 ? HT : 1], vh[HT > 0 ? HT : 1], vv[HT > 0 ? HT : 1], vd[HT > 0 ? HT : 1];
 #pragma unroll
                     for (int qq = 0; qq < HT; ++qq) {
-                        va[qq] = cA[b0 - qq];
-                        vv[qq] = cV[b0 - qq];
-                        vh[qq] = cH[b0 - qq];
-                        vd[qq] = cD[b0 - qq];
+                        va[qq] = tA(cA[b0 - qq]);
+                        vv[qq] = tl(cV[b0 - qq]);
+                        vh[qq] = tl(cH[b0 - qq]);
+                        vd[qq] = tl(cD[b0 - qq]);
                     }
                     sm_order<HT>(c1, plain, [&](int j) { return make_float2(va[j], vh[j]); },
                                  [&](int j) { return staps[2][2 * j + par]; },
@@ -862,14 +872,14 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                     for (int qq = 0; qq < HH; ++qq) {
                         int ci;
                         const int sl = sm_syn_tap(sy, sc, Nc, qq, &ci);
-                        lo = lo + staps[2][ci] * cA[rb0 + sl];
-                        hi = hi + staps[2][ci] * cH[rb0 + sl];
+                        lo = lo + staps[2][ci] * tA(cA[rb0 + sl]);
+                        hi = hi + staps[2][ci] * tl(cH[rb0 + sl]);
                     }
                     for (int qq = 0; qq < HH; ++qq) {
                         int ci;
                         const int sl = sm_syn_tap(sy, sc, Nc, qq, &ci);
-                        lo = lo + staps[3][ci] * cV[rb0 + sl];
-                        hi = hi + staps[3][ci] * cD[rb0 + sl];
+                        lo = lo + staps[3][ci] * tl(cV[rb0 + sl]);
+                        hi = hi + staps[3][ci] * tl(cD[rb0 + sl]);
                     }
                 }
                 LoHi[e] = make_float2(lo, hi);

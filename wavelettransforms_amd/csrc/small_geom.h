@@ -173,7 +173,8 @@ WT_SM SmNeed sm_need(const SmAxis& ar, const SmAxis& ac, int32_t L, int32_t F) {
 
 /* regions start 16-byte aligned: up to 3 words of padding after each of the first three */
 WT_SM int32_t sm_fwd_words(const SmNeed& n) { return n.fkeys + n.fx + n.flh + 12; }
-/* the select gathers up to 64 slots of 128 words at the arena's tail while the windows are live */
-WT_SM int32_t sm_inv_words(const SmNeed& n) { return n.fkeys + n.iwin + n.ia + n.ilh + 16 + 64 * 128; }
+/* the select gathers the segment's key slots (SM_SEG_WG_MAX x SM_SLOT_WORDS = 8192 words) at the
+ * arena's tail while the windows are live */
+WT_SM int32_t sm_inv_words(const SmNeed& n) { return n.fkeys + n.iwin + n.ia + n.ilh + 16 + 8192; }
 
 #endif

@@ -210,13 +210,13 @@ void launch_resident(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_res
  * every tensor of the call is a 2-D transform whose tiles fit one workgroup's LDS; one
  * workgroup per tile, the tiles of a tensor are its segment (small_geom.h) */
 constexpr int SM_MAX_SEG = 4;       /* tensors per call */
-constexpr int SM_SEG_WG_MAX = 64;   /* workgroups per tensor */
-constexpr int SM_SLOT_WORDS = 128;  /* per workgroup in the candidate region: the keys of the rank's bin */
+constexpr int SM_SEG_WG_MAX = 128;  /* workgroups per tensor */
+constexpr int SM_SLOT_WORDS = 64;   /* per workgroup in the candidate region: the keys of the rank's bin */
 constexpr int SM_ARENA = 34 * 1024; /* LDS words of a workgroup's arena (136 KB) */
 constexpr int SM_F_MAX = 20;        /* longest filter */
 constexpr int SM_LMAX = 10;         /* = SM_MAX_L of small_geom.h */
 constexpr int SM_WIN_WORDS = 480;   /* the tiles' windows, computed by the host (small_geom.h): per tile row
-                                       and per tile column 3 (L + 1) words, level k's fw, sv and own range */
+                                       and per tile column 2 (L + 1) words, level k's fw and sv */
 constexpr int SM_LINE_MAX = 32767;  /* window ends packed in 16 bits */
 struct SmallSeg {
     const float* in;
