@@ -23,6 +23,10 @@ echo "== rehearsal --gpus 2"; WTP_BENCH_REHEARSAL=1 timeout -k 10 300 python ben
 grep '"metric"' "$OUT/bench_n2_$TAG.log" | cut -c1-400
 echo "== rocprof cfg2"; cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 400 --warmup 5 --no-cpu --no-cold --no-rocprof > "$OUT/bench_prof_$TAG.log" 2>&1 || { echo rocprof failed; tail -30 "$OUT/bench_prof_$TAG.log"; exit 1; }
 head -3 "$OUT/prof_$TAG/run_kernel_stats.csv" | cut -c1-200
+echo "== rocprof cfg3"; cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof3_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg3 --steps 400 --warmup 5 --no-cpu --no-cold --no-rocprof > "$OUT/bench_prof3_$TAG.log" 2>&1 || { echo rocprof cfg3 failed; tail -30 "$OUT/bench_prof3_$TAG.log"; exit 1; }
+head -3 "$OUT/prof3_$TAG/run_kernel_stats.csv" | cut -c1-200
 echo "== pmc cfg2"; cd "$ROOT" && timeout -k 10 600 bash tools/pmc_run.sh "$TAG" > "$OUT/pmc_$TAG.log" 2>&1 || { echo pmc failed; tail -20 "$OUT/pmc_$TAG.log"; exit 1; }
 python3 tools/pmc_summary.py "$OUT/pmc_$TAG" "$OUT/pmc_${TAG}_cfg2.json" "$TAG" || exit 1
+echo "== pmc cfg3"; timeout -k 10 600 bash tools/pmc_run.sh "${TAG}c3" --config cfg3 > "$OUT/pmc_${TAG}c3.log" 2>&1 || { echo pmc cfg3 failed; tail -20 "$OUT/pmc_${TAG}c3.log"; exit 1; }
+python3 tools/pmc_summary.py "$OUT/pmc_${TAG}c3" "$OUT/pmc_${TAG}_cfg3.json" "${TAG}c3" || exit 1
 echo done
