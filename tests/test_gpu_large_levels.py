@@ -1,0 +1,44 @@
+"""Large analysis levels at shapes the golden cases do not reach: several tiles across and down,
+odd extents (periodization's repeated last sample), partial last tiles, the right-edge split order,
+batch dimensions and two depths.  Packed coefficients (pywt.wavedec2 + coeffs_to_array,
+ResNet/dwt_pruning.py:67-72) and the pruned outputs must equal the oracle bit for bit for every
+filter length the filter bank specialises."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests import golden_io as G
+from wavelettransforms_amd import engine as eng
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+
+
+# F = 2, 4, 6, 8, 10, 12, 16, 18: every specialised filter length
+WAVELETS = ["haar", "db2", "rbio2.2", "bior3.3", "db5", "coif2", "db8", "db9"]
+# odd extents (4-D, as the reference's crop needs), a last tile row of one output row (R = 130),
+# a last tile a few columns wide
+SHAPES = [(1, 1, 130, 1001), (2, 1, 255, 520), (1, 3, 301, 777), (512, 1024), (999, 600)]
+
+
+@pytest.mark.parametrize("wavelet", WAVELETS)
+def test_large_levels_equal_oracle(wavelet):
+    for j, shp in enumerate(SHAPES):
+        e = G.W.sigma_exponent((2.0 / (shp[-1] * shp[-2])) ** 0.5)
+        host = G.W.synth_numpy(shp, 31, j, e)
+        x = eng.synth(shp, 31, j, e)
+        for level in (1, 3):
+            P = eng.wavedec2_packed(x, wavelet, level).cpu().numpy()
+            assert np.array_equal(P.view(np.uint32), O.wavedec2_packed(host, wavelet, level).view(np.uint32)), \
+                (shp, level)
+            if len(shp) == 2 and (shp[0] % 2 or shp[1] % 2):
+                continue  # odd 2-D: the reference's crop raises (dwt_pruning.py:79-82)
+            ref, rr = O.prune_tensor(host, wavelet, level, 37.5)
+            outs, (r,) = eng.prune([x], wavelet, level, 37.5)
+            assert np.array_equal(outs[0].cpu().numpy(), ref), (shp, level)
+            assert r["zero_count"] == rr["zero_count"] and G.f64_bits_equal(r["thr64"], rr["thr64"])

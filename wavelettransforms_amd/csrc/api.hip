@@ -106,7 +106,11 @@ bool pct_ok(double pct) { return pct >= 0.0 && pct <= 100.0; }
  * than k_collect saved).  The resident form always uses NSUB_MAX buckets: its runs are per
  * workgroup, and narrow buckets let one LDS histogram finish the select. */
 void bucket_plan(int64_t n, int* nsub_log2, int* bucket_cap, bool dwt) {
-    const double expect = 0.05 * (double)n;
+    /* a segment too large for the inline window always gets k_window's M_SAMPLE_WIN-key window:
+     * 2 (6 sigma + 24) sample ranks wide, plus the bins' outward rounding */
+    const double m = (double)M_SAMPLE_WIN;
+    const double wfrac = n > (int64_t)WINDOW_INLINE_MAX_BLOCKS * CHUNK ? (6.0 * sqrt(m) + 48.0) / m + 0.005 : 0.05;
+    const double expect = wfrac * (double)n;
     int lg = 6;
     while (lg < 10 && (double)(1 << lg) * (dwt ? 2048.0 : 1024.0) < expect) ++lg;
     int64_t bc = (int64_t)(4.0 * expect / (double)(1 << lg)) + 1;

@@ -248,6 +248,9 @@ struct WindowLds {
  * the window: kl = low edge of the bin of the lower bracket (0: open), kh = high edge of the
  * bin of the upper bracket (0xFFFFFFFF: open), and the bucket shift for nsub buckets. */
 template <int THREADS, int MS>
+__device__ __forceinline__ void window_search(const SegDesc& sd, WindowLds<THREADS>& L, uint32_t* kl_out,
+                                              uint32_t* kh_out, uint32_t* sh_out);
+template <int THREADS, int MS>
 __device__ __forceinline__ void window_from_keys(const SegDesc& sd, const uint32_t (&k)[MS / THREADS],
                                                  WindowLds<THREADS>& L, uint32_t* kl_out, uint32_t* kh_out,
                                                  uint32_t* sh_out) {
@@ -264,6 +267,17 @@ __device__ __forceinline__ void window_from_keys(const SegDesc& sd, const uint32
         if (j * THREADS + (int)threadIdx.x < m) atomicAdd(&L.h[key_bin(k[j])], 1u);
     __syncthreads();
     WTP_WPROBE(1);
+    window_search<THREADS, MS>(sd, L, kl_out, kh_out, sh_out);
+}
+
+/* the search half: L.h holds the histogram of the MS sampled keys (all n when n <= MS) */
+template <int THREADS, int MS>
+__device__ __forceinline__ void window_search(const SegDesc& sd, WindowLds<THREADS>& L, uint32_t* kl_out,
+                                              uint32_t* kh_out, uint32_t* sh_out) {
+    constexpr int FBP = WindowLds<THREADS>::FBP;
+    const int64_t n = sd.n;
+    const bool exact = n <= MS;
+    const int m = exact ? (int)n : MS;
     /* sample ranks fit 32 bits; the bin counts stay in registers from the scan to the search */
     const int64_t r0 = sd.r0, r1 = sd.above ? sd.r0 : sd.r0 + 1;
     int sa, sb;
@@ -892,10 +906,34 @@ constexpr int WIN_THREADS = 1024;
 __global__ __launch_bounds__(WIN_THREADS) void k_window(SegTable t, SelHeader* __restrict__ head) {
     __shared__ WindowLds<WIN_THREADS> wl;
     const SegDesc& sd = t.s[blockIdx.x];
-    uint32_t ks[M_SAMPLE_WIN / WIN_THREADS];
-    sample_keys<WIN_THREADS, M_SAMPLE_WIN>(sd, ks);
+    /* the sample in passes of 16 keys a thread (groups of SAMPLE_GROUP contiguous keys spread
+     * evenly over the segment, as sample_keys), histogrammed as they arrive */
+    constexpr int PASS = 16 * WIN_THREADS, NPASS = M_SAMPLE_WIN / PASS;
+    static_assert(M_SAMPLE_WIN % PASS == 0, "sample passes");
+    for (int i = threadIdx.x; i < WindowLds<WIN_THREADS>::FBP * WIN_THREADS; i += WIN_THREADS) wl.h[i] = 0;
+    if (threadIdx.x < 2) wl.found[threadIdx.x] = -1;
+    __syncthreads();
+    {
+        const int64_t n = sd.n;
+        const bool exact = n <= M_SAMPLE_WIN;
+        const double step = exact ? 0.0 : (double)(n - SAMPLE_GROUP) / (double)(M_SAMPLE_WIN / SAMPLE_GROUP - 1);
+        for (int ps = 0; ps < NPASS; ++ps) {
+            uint32_t k[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int i = ps * PASS + j * WIN_THREADS + (int)threadIdx.x;
+                const int64_t pos = exact ? min((int64_t)i, n - 1)
+                                          : (int64_t)((double)(i / SAMPLE_GROUP) * step) + (i % SAMPLE_GROUP);
+                k[j] = abs_key(sd.data[pos]);
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (!exact || ps * PASS + j * WIN_THREADS + (int)threadIdx.x < n) atomicAdd(&wl.h[key_bin(k[j])], 1u);
+        }
+    }
+    __syncthreads();
     uint32_t kl, kh, sh;
-    window_from_keys<WIN_THREADS, M_SAMPLE_WIN>(sd, ks, wl, &kl, &kh, &sh);
+    window_search<WIN_THREADS, M_SAMPLE_WIN>(sd, wl, &kl, &kh, &sh);
     if (threadIdx.x == 0) {
         SelState* st = sel_region(head, head->parity) + sd.slot;
         st->kl = kl;

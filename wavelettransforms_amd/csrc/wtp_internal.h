@@ -22,8 +22,13 @@ namespace wtp {
  * ranks and resolves them exactly, or by a full radix select over the segment if the window
  * missed. */
 constexpr int M_SAMPLE = 4096;      /* k_resident: every workgroup draws it before its chunk    */
-constexpr int M_SAMPLE_WIN = 16384; /* k_window (three-launch form): one block per segment; the
-                                       narrower window halves k_collect's candidate traffic */
+#ifndef WTP_SAMPLE_WIN
+#define WTP_SAMPLE_WIN 65536
+#endif
+/* k_window (three-launch form): one block per segment, 64 keys a thread in passes of 16; on cfg5
+ * 65536 keys (window ~2.4 % of the segment) beat 16384 (~5 %: k_collect +55 us per 24-segment
+ * launch) and 262144 (~1.2 %: k_window +47 us for 10 us less k_collect) */
+constexpr int M_SAMPLE_WIN = WTP_SAMPLE_WIN;
 constexpr int SAMPLE_GROUP = 16;   /* contiguous keys per sample group */
 constexpr int NSUB_MAX = 1024;     /* buckets over (kl, kh]: 64..1024 per segment (SegDesc) */
 constexpr int RES_NSUB_LOG2 = 10;  /* k_resident: 1024 buckets over (kl, kh] (4096 measured slower: 8 KB more reads per workgroup) */
