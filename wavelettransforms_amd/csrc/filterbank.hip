@@ -45,6 +45,10 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr int FB_THREADS = 256;
 constexpr int FR = 16, FC = 64;  /* forward output tile (per subband) */
 constexpr int IR = 64, IC = 64;  /* inverse output tile */
+#ifndef WTP_INV_RG
+#define WTP_INV_RG 2
+#endif
+constexpr int INV_RG = WTP_INV_RG; /* synthesis row-pass rows interleaved per wave */
 constexpr int FB_MAX_LDS = 64 * 1024;
 
 /* XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (blocks b and b+8
@@ -570,13 +574,45 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
             if (__all(!s.special && s.i < a.C)) {
                 /* interior columns: no branch between the rows (rows past NRr are clamped, computed
                  * and dropped at the write), so their independent sums interleave */
+                /* INV_RG rows at a time, tap-major: their chains are independent, so they
+                 * interleave instead of running one 2H-long dependent chain after another */
+                constexpr int G = INV_RG;
 #pragma unroll
-                for (int q = 0; q < RRN; ++q) {
-                    const int rr = min(wv + 4 * q, NRr - 1);
-                    f2 acc = {0.0f, 0.0f};
-                    acc = syn_pass_inner<FT>(s, F, tl_, getA(rr), acc);
-                    acc = syn_pass_inner<FT>(s, F, th_, getD(rr), acc);
-                    rowres[q] = acc;
+                for (int q0 = 0; q0 < RRN; q0 += G) {
+                    f2 acc[G], v[G][HM];
+                    int rb[G];
+#pragma unroll
+                    for (int gq = 0; gq < G; ++gq) {
+                        acc[gq] = f2{0.0f, 0.0f};
+                        rb[gq] = min(wv + 4 * min(q0 + gq, RRN - 1), NRr - 1) * NCc + s.iu - c_lo;
+                    }
+#pragma unroll
+                    for (int gq = 0; gq < G; ++gq)
+#pragma unroll
+                        for (int j = 0; j < HM; ++j) {
+                            const float2 t = Aq[rb[gq] - j];
+                            v[gq][j] = f2{t.x, t.y};
+                        }
+#pragma unroll
+                    for (int j = 0; j < HM; ++j)
+#pragma unroll
+                        for (int gq = 0; gq < G; ++gq)
+                            if (q0 + gq < RRN) acc[gq] = acc[gq] + tlo[j] * v[gq][j];
+#pragma unroll
+                    for (int gq = 0; gq < G; ++gq)
+#pragma unroll
+                        for (int j = 0; j < HM; ++j) {
+                            const float2 t = Dq[rb[gq] - j];
+                            v[gq][j] = f2{t.x, t.y};
+                        }
+#pragma unroll
+                    for (int j = 0; j < HM; ++j)
+#pragma unroll
+                        for (int gq = 0; gq < G; ++gq)
+                            if (q0 + gq < RRN) acc[gq] = acc[gq] + thi[j] * v[gq][j];
+#pragma unroll
+                    for (int gq = 0; gq < G; ++gq)
+                        if (q0 + gq < RRN) rowres[q0 + gq] = acc[gq];
                 }
             } else {
 #pragma unroll
@@ -637,23 +673,36 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
                 float2 r[NV];
 #pragma unroll
                 for (int q = 0; q < NV; ++q) r[q] = LoHi[(g0 + q) * IC + lane];
+                /* tap-major over the RB2 output pairs: RB2 independent chains interleave, and
+                 * each tap is read once per j (two parities) instead of once per output */
+                f2 acc[RB2];
+#pragma unroll
+                for (int k = 0; k < RB2; ++k) acc[k] = f2{0.0f, 0.0f};
+#pragma unroll
+                for (int j = 0; j < H; ++j) {
+                    const float t0 = rlo[2 * j], t1 = rlo[2 * j + 1];
+#pragma unroll
+                    for (int k = 0; k < RB2; ++k) {
+                        const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
+                        const float t = par ? t1 : t0;
+                        acc[k] = acc[k] + f2{t, t} * f2{r[base - j].x, r[base - j + RB2 / 2].x};
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < H; ++j) {
+                    const float t0 = rhi[2 * j], t1 = rhi[2 * j + 1];
+#pragma unroll
+                    for (int k = 0; k < RB2; ++k) {
+                        const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
+                        const float t = par ? t1 : t0;
+                        acc[k] = acc[k] + f2{t, t} * f2{r[base - j].y, r[base - j + RB2 / 2].y};
+                    }
+                }
 #pragma unroll
                 for (int k = 0; k < RB2; ++k) {
-                    const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
-                    f2 acc = {0.0f, 0.0f};
-#pragma unroll
-                    for (int j = 0; j < H; ++j) {
-                        const float t = rlo[2 * j + par];
-                        acc = acc + f2{t, t} * f2{r[base - j].x, r[base - j + RB2 / 2].x};
-                    }
-#pragma unroll
-                    for (int j = 0; j < H; ++j) {
-                        const float t = rhi[2 * j + par];
-                        acc = acc + f2{t, t} * f2{r[base - j].y, r[base - j + RB2 / 2].y};
-                    }
-                    yb[(int64_t)(nf + k) * a.outW + m] = acc.x;
-                    yb[(int64_t)(nf + k + RB2) * a.outW + m] = acc.y;
-                    z += (acc.x == 0.0f) + (acc.y == 0.0f);
+                    yb[(int64_t)(nf + k) * a.outW + m] = acc[k].x;
+                    yb[(int64_t)(nf + k + RB2) * a.outW + m] = acc[k].y;
+                    z += (acc[k].x == 0.0f) + (acc[k].y == 0.0f);
                 }
             }
         }
