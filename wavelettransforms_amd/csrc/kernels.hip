@@ -2179,12 +2179,15 @@ static bool window_inline(const SegTable& t) { return collect_blocks(t) <= WINDO
 void launch_window(const SegTable& t, SelHeader* head, hipStream_t s) {
     if (!window_inline(t)) hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, s, t, head);
 }
+#ifndef WTP_COLLECT_LAB /* lab ablations only (1: stop after the counters, 2: after the bucket histogram) */
+#define WTP_COLLECT_LAB 0
+#endif
 void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s) {
     if (window_inline(t))
         hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT, true>), dim3(collect_blocks(t)),
                            dim3(COLLECT_THREADS), 0, s, t, head, cand, res);
     else
-        hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT, false>), dim3(collect_blocks(t)),
+        hipLaunchKernelGGL((k_collect_t<WTP_COLLECT_LAB, COLLECT_THREADS, COLLECT_IT, false>), dim3(collect_blocks(t)),
                            dim3(COLLECT_THREADS), 0, s, t, head, cand, res);
 }
 void launch_minprune(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
