@@ -115,6 +115,26 @@ def test_degenerate_data(kind):
         _same(outs[0].cpu().numpy(), ref, r, rr)
 
 
+@pytest.mark.parametrize("split", ["columns", "rows", "one_tile"])
+def test_tile_local_distributions_differ(split):
+    """Tiles whose local |c| distributions sit far from the segment's: their speculative slots
+    (the bins around each tile's local estimate of the ranks, published before barrier 0) miss
+    the rank's bin, so the select falls back to the per-bin slots behind barrier 1 -- results
+    still equal the oracle and the multi-launch form."""
+    host = G.W.synth_numpy((128, 784), 11, 0, 26)
+    if split == "columns":
+        host[:, : host.shape[1] // 2] *= np.float32(1e3)
+    elif split == "rows":
+        host[host.shape[0] // 3:] *= np.float32(1e-3)
+    else:
+        host[:16, :64] *= np.float32(1e4)
+    for pct in (50.0, 10.0, 90.0):
+        ref, rr = O.prune_tensor(host, "rbio2.2", 3, pct)
+        outs, (r,) = _both([_dev(host)], "rbio2.2", 3, pct)
+        assert r["path"] == eng.MODE_SMALL
+        _same(outs[0].cpu().numpy(), ref, r, rr)
+
+
 def test_in_place():
     host = G.W.synth_numpy((128, 784), 3, 0, 26)
     xt = _dev(host)
