@@ -982,12 +982,18 @@ __global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelHeader* __restr
             collect_body<CT, IT, false, LAB, WIN>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
     }
     __syncthreads(); /* every wave has read the parity */
+    /* the grid's last block flips the parity (visible to the next kernel at the boundary).  Its
+     * count is sharded (blockIdx % 8; the last block of a shard adds to the top counter, as in
+     * k_small): one returning add per block on a single address queued ~25K blocks of a cfg5
+     * launch behind each other.  The counters sit in this region's BarState, zero at the start
+     * of the launch (the previous launch cleared it as its idle region). */
     if (threadIdx.x == 0) {
-        const uint32_t d = atomicAdd(&head->done, 1u);
-        if (d == gridDim.x - 1) { /* last block: visible to the next kernel at the boundary */
-            head->done = 0;
+        BarState* br = bar_region(head, q);
+        const uint32_t sh = blockIdx.x & (NSHARD - 1);
+        const uint32_t nsh = (gridDim.x - sh + NSHARD - 1) / NSHARD; /* blocks of this shard */
+        const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);     /* shards with blocks */
+        if (atomicAdd(&br->arrive[sh][0], 1u) == nsh - 1u && atomicAdd(&br->arrive[0][16], 1u) == nact - 1u)
             head->parity = q ^ 1u;
-        }
     }
 }
 
