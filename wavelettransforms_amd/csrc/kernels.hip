@@ -197,6 +197,9 @@ __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, i
 #ifndef WTP_RES_CNT /* k_resident's below / == kl counts: 1 ballot popcounts (scalar unit), 0 per-lane */
 #define WTP_RES_CNT 0
 #endif
+#ifndef WTP_RES_FLIP_SHARD /* k_resident's parity flip: 1 sharded counters off the polling lane, 0 one counter */
+#define WTP_RES_FLIP_SHARD 1
+#endif
 #ifndef WTP_RES_SPEC /* k_resident: speculative stores of the decided keys during the second barrier */
 #define WTP_RES_SPEC 0
 #endif
@@ -1430,8 +1433,21 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     uint32_t* b1 = reinterpret_cast<uint32_t*>(&st->seg_bar[1]);
     uint32_t* b2 = reinterpret_cast<uint32_t*>(&st->seg_bar[2]);
     res_arrive(b1);
-    /* the grid's last arrival flips the region parity (every workgroup has read it by then) */
+    /* the grid's last arrival flips the region parity (every workgroup has read it by then):
+     * lane 0 of wave 1, off the polling lane's path, through per-shard counters (blockIdx % 8;
+     * the last arriver of a shard adds to the top counter) so no address queues more than
+     * ~gridDim / 8 returning adds */
+#if WTP_RES_FLIP_SHARD
+    if (tid == 64) {
+        const uint32_t sh8 = blockIdx.x & (NSHARD - 1);
+        const uint32_t nsh = (gridDim.x - sh8 + NSHARD - 1) / NSHARD;
+        const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);
+        if (atomicAdd(&bar->arrive[sh8][0], 1u) == nsh - 1u && atomicAdd(&bar->arrive[0][16], 1u) == nact - 1u)
+            stc(&head->parity, q ^ 1u);
+    }
+#else
     if (tid == 0 && atomicAdd(&bar->arrive[0][0], 1u) == gridDim.x - 1u) stc(&head->parity, q ^ 1u);
+#endif
     WTP_RPROBE(4);
     if (!res_wait(b1, nwg, tmo)) {
         if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
