@@ -129,6 +129,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ragged_rsrc(const float* p, in
 template <int IT, int CT = STREAM_THREADS>
 __device__ __forceinline__ void load_chunk_ragged(const float* p, int len, float4 (&v)[IT]) {
     const __amdgpu_buffer_rsrc_t r = ragged_rsrc(p, len);
+    if ((reinterpret_cast<uintptr_t>(p) & 15) == 0 && (len & 3) == 0) { /* uniform */
+        /* every float4 lies wholly inside or wholly past len: one 16-byte range-checked load
+         * each (past len it reads as zeros) instead of four dword loads */
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const u4 q = __builtin_amdgcn_raw_buffer_load_b128(r, 16 * (it * CT + (int)threadIdx.x), 0, 0);
+            v[it] = make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w));
+        }
+        return;
+    }
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
         const int e = 4 * (it * CT + (int)threadIdx.x);
