@@ -998,9 +998,9 @@ __global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelHeader* __restr
     __syncthreads(); /* every wave has read the parity */
     /* the grid's last block flips the parity (visible to the next kernel at the boundary).  Its
      * count is sharded (blockIdx % 8; the last block of a shard adds to the top counter, as in
-     * k_small): one returning add per block on a single address queued ~25K blocks of a cfg5
-     * launch behind each other.  The counters sit in this region's BarState, zero at the start
-     * of the launch (the previous launch cleared it as its idle region). */
+     * k_small), so no single word takes a returning add from each of a cfg5 launch's ~25K blocks
+     * (measured ~1 % of k_collect).  The counters sit in this region's BarState, zero at the
+     * start of the launch (the previous launch cleared it as its idle region). */
     if (threadIdx.x == 0) {
         BarState* br = bar_region(head, q);
         const uint32_t sh = blockIdx.x & (NSHARD - 1);
