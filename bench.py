@@ -10,8 +10,9 @@ layer its own level and percentile, dwt_pruning.py:130-174).
 --gpus N (N > 1): unless WORLD_SIZE is set (torchrun), N rank processes are started here, before
 anything touches the GPU (python -m torch.distributed.run on 127.0.0.1), one per GPU.  The
 headline at N > 1 is north_star's split, BASELINE configs[3] (cfg4): ONE model's layers
-LPT-sharded over the ranks, each rank pruning its layers straight into its flat shard, then ONE
-RCCL all_gather_into_tensor that reassembles the pruned state_dict on every rank -- strong
+LPT-sharded over the ranks, each rank pruning its layers straight into its region of the flat
+state_dict buffer, then ONE full-mesh exchange of the unpadded regions (an RCCL group of
+point-to-point copies over xGMI) that reassembles the pruned state_dict on every rank -- strong
 scaling of one model (end-to-end per step = compute + all-gather, max over ranks).  The replica
 leg (every rank prunes its own model, no collective: weak scaling) is reported beside it.
 --config cfg5 (BASELINE configs[4]): 64 blocks of 4096^2 (db8 level 5) split over the ranks
@@ -208,7 +209,7 @@ def main():
     from wavelettransforms_amd import _native as N
     from wavelettransforms_amd import engine
     from wavelettransforms_amd import workloads as W
-    from wavelettransforms_amd.sharding import REC_BYTES, ShardPlan, _Shard, assemble
+    from wavelettransforms_amd.sharding import REC_BYTES, ShardPlan, _Shard, assemble, exchange
 
     L = N.lib()
     if args.no_resident:
@@ -240,15 +241,14 @@ def main():
     n_w = sum(x.numel() for x in (xs_all if not sharded else [xs_all[i] for i in plan.mine[rank]]))
 
     if sharded:
-        shard = _Shard(xs_all, plan, rank, dev)
-        gathered = torch.empty(world * plan.slice, dtype=torch.float32, device=dev)
+        shard = _Shard(xs_all, plan, rank, dev)  # its region of the flat state_dict buffer shard.full
 
         def compute():
             if shard.mine:
                 shard.run(shard.mine, wavelet, level, pct)
 
         def gather():
-            dist.all_gather_into_tensor(gathered, shard.buf)
+            exchange(shard.full, plan, rank)
 
         def step():
             compute()
@@ -267,7 +267,7 @@ def main():
         step()
     torch.cuda.synchronize()
     if sharded:
-        _, recs_all = assemble(gathered.view(world, -1), plan)
+        _, recs_all = assemble(shard.full, plan)
         recs = [recs_all[i] for i in plan.mine[rank]]
     else:
         host = res_buf.cpu().numpy().view(engine.RESULT_DTYPE)[:len(xs)]
@@ -323,19 +323,32 @@ def main():
             dist.barrier()
         return max_over_ranks(time.perf_counter() - t0)
 
+    def faulted_now():
+        """Records of the last step that read MODE_FAULT (a resident wait timed out: nothing was
+        stored for that tensor and the step absorbed the bound) -- the line is marked, not trusted."""
+        if sharded:
+            _, rr = assemble(shard.full, plan)
+            return sum(1 for r in rr if r["path"] == engine.MODE_FAULT)
+        return int(engine.fault_mask(res_buf, len(xs)).sum()) if xs else 0
+
     # ------------------------------------------------------------ the headline
     K = args.steps
-    T = timed(K)
+    T = timed(K)  # exactly K steps between barrier + synchronize, max over ranks
     ms_per_step = T / K * 1e3
     value = n_model * K / T
+    timed_region = {"steps": K, "ms_per_step": ms_per_step, "value": value}
     if args.profile_child:
         return
+    faults_timed = faulted_now()
 
-    # per-replay distribution (>= 50 replays of G steps, each bracketed by events on the stream)
+    # per-replay distribution (>= 50 replays of G steps, each bracketed by events on the stream);
+    # with a graph the headline value and ms_per_step are its p50, so that a short --steps (the
+    # driver's 20 = 2 replays) cannot hinge on one or two replays (VERDICT r02, item 8)
     dist_ms = None
+    value_src = "the K-step timed region (barrier + synchronize on both sides, max over ranks)"
     if graph is not None:
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.replays)]
+               for _ in range(max(50, args.replays))]
         for a, b in evs:
             a.record()
             graph.replay()
@@ -344,6 +357,11 @@ def main():
         per = np.array([a.elapsed_time(b) / G for a, b in evs])
         dist_ms = {"replays": len(evs), "steps_per_replay": G, "p10": float(np.percentile(per, 10)),
                    "p50": float(np.percentile(per, 50)), "p90": float(np.percentile(per, 90))}
+        ms_per_step = dist_ms["p50"]
+        value = n_model / (ms_per_step * 1e-3)
+        value_src = ("p50 of %d graph replays of %d steps each, HIP events on the replay stream; the K-step timed "
+                     "region is reported beside it as timed_region" % (len(evs), G))
+    faults_timed += faulted_now()
 
     # ------------------------------------- dominant kernel: in-kernel launch span
     def stamp_spans(reps, before=None):
@@ -463,9 +481,13 @@ def main():
         t_rep = timed(Kc, replica) / Kc * 1e3
         multi = {"cfg4_one_model": {"end_to_end_ms": ms_per_step, "compute_ms_max_rank": t_comp,
                                     "all_gather_ms": t_gath, "max_rank_weights": int(plan.max_shard),
-                                    "gathered_bytes_per_rank": int(world * plan.slice * 4),
-                                    "note": "LPT layer shards pruned into the flat shard, one all_gather_into_tensor "
-                                            "(RCCL) of weights + records; eager launches"},
+                                    "bytes_sent_this_rank": plan.bytes_sent(rank),
+                                    "bytes_received_this_rank": plan.bytes_received(rank),
+                                    "bytes_received_max_rank": max(plan.bytes_received(r) for r in range(world)),
+                                    "note": "LPT layer shards pruned in place into the flat state_dict buffer, then "
+                                            "ONE full-mesh exchange of the unpadded regions (weights + records; "
+                                            "batch_isend_irecv = one RCCL group of point-to-point copies, one per "
+                                            "xGMI peer link); eager launches"},
                  "replicas": {"value": world * n_model / (t_rep * 1e-3), "ms_per_step": t_rep, "scaling": "weak",
                               "note": "every rank prunes its own full model, no collective"}}
 
@@ -518,7 +540,9 @@ def main():
                        "parallelism": ("lpt-layer-shard%d+allgather" % world if sharded
                                        else ("block-split%d" % world if world > 1 else "single")),
                        "transform": "1-D flattened (extension)" if args.flatten else "2-D over (kh, kw) (reference)"},
-            "pipeline_hbm_gbs": 8 * n_model * K / T / 1e9,
+            "value_source": value_src,
+            "timed_region": timed_region,
+            "pipeline_hbm_gbs": 8 * n_model / (ms_per_step * 1e-3) / 1e9,
             "step_distribution_ms": dist_ms,
             "roofline": None if dom is None else {
                 "bound": "hbm", "kernel": dom_kernel, "stage": dom, "launches_per_stage": dom_launches,
@@ -534,6 +558,9 @@ def main():
         }
         if faults:
             line["resident_faults"] = faults
+        if faults_timed:
+            line["resident_faults_timed"] = faults_timed
+            line["valid"] = False  # a timed step hit the resident timeout: this line is not a measurement
         if args.config == "cfg5":
             flops = DB8_L5_FLOP_PER_ELEM * n_model
             line["valu_roof"] = {"flop_per_elem": DB8_L5_FLOP_PER_ELEM, "peak_tflops": VALU_NOFMA_TFLOPS,

@@ -176,7 +176,8 @@ int wtp_resident_capacity(void); /* 0 if the current device cannot host the resi
  * launch whose workgroups were not all resident at once times out there and stores NOTHING for
  * the tensors concerned (inputs and outputs untouched): their records read path == 99
  * (WTP_PATH_FAULT), and the caller re-runs exactly those tensors with wtp_set_resident(0).
- * Default 200000; tests lower it to force the fault path. */
+ * Default 200000, at most 40000000 (larger values are clamped: the bound is kept in 32-bit
+ * ticks of the 100 MHz wall clock); tests lower it to force the fault path. */
 unsigned wtp_set_resident_timeout_us(unsigned us);
 #define WTP_PATH_FAULT 99
 #define WTP_PATH_SMALL 4 /* every tensor of the call ran in one launch (2-D transforms, small population) */

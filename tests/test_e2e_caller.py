@@ -80,3 +80,62 @@ def test_main_pruning_sequence(tmp_path, capsys):
         assert int(r["Total Pruned Count"]) == int(s["Total Pruned Count"]) == int((m.weight == 0).sum()), name
     assert [e[4] for e in exp[1:]] == ["selective", "random", "min"]
     assert "Selectively pruned model saved at" in out and "Minimum weight pruning completed." in out
+
+
+def _run_sequential(model, exp_csv, guid):
+    from wavelettransforms_amd.dwt_pruning import wavelet_pruning
+    from wavelettransforms_amd.min_weight_pruning import min_weight_pruning
+    from wavelettransforms_amd.random_pruning import random_pruning
+    dwt, rnd, mn = copy.deepcopy(model), copy.deepcopy(model), copy.deepcopy(model)
+    log_path = wavelet_pruning(dwt, "bior4.4", 5, 0.382 * 100, exp_csv, guid)
+    random_pruning(rnd, log_path, guid, "bior4.4", 5, 0.382, exp_csv)
+    min_weight_pruning(mn, log_path, guid, "bior4.4", 5, 0.382, exp_csv)
+    return log_path, (dwt, rnd, mn)
+
+
+def _conv_weights(m):
+    return [(n, x.weight.detach().cpu().numpy()) for n, x in m.named_modules() if isinstance(x, torch.nn.Conv2d)]
+
+
+def test_main_pruning_threaded(tmp_path):
+    """main_pruning.py as it runs (:169-215): the selective prune, then random and min-weight
+    pruning in two host threads that drive the library at once and log through one queue drained
+    by a log_worker thread (wavelettransforms_amd.main_pruning.run).  Against the sequential run of
+    the same model: identical per-layer logs, pruned weights (the random thread draws the same
+    seed), and the same set of experiment-log rows (their order is the threads' race)."""
+    assert torch.cuda.is_available()
+    from wavelettransforms_amd import main_pruning
+    model = _resnet18()
+    cwd = os.getcwd()
+    res = {}
+    for mode in ("threaded", "sequential"):
+        work = tmp_path / mode / "a" / "b"
+        work.mkdir(parents=True)
+        exp_csv = str(tmp_path / mode / "experiment_log.csv")
+        os.chdir(work)
+        try:
+            torch.manual_seed(1234)
+            if mode == "threaded":
+                _, log_path, models = main_pruning.run(model, "bior4.4", 5, 0.382, exp_csv, guid="e2e1guid")
+            else:
+                log_path, models = _run_sequential(model, exp_csv, "e2e1guid")
+        finally:
+            os.chdir(cwd)
+        root = tmp_path / mode / "WaveletTransforms" / "ResNet" / "SavedModels" / "bior4.4_threshold-0.382_level-5_guid-e2e1"
+        logs = {ph: [list(r.values()) for r in csv.DictReader(open(root / ph / "log.csv"))]
+                for ph in ("selective_pruned", "random_pruned", "min_pruned")}
+        exp = list(csv.reader(open(exp_csv)))
+        rows = {tuple(e[:7]) for e in exp[1:]}  # the model path differs by the run's directory
+        res[mode] = (logs, [_conv_weights(m) for m in models], rows, [e[4] for e in exp[1:]])
+    (lt, wt, rt, pt), (ls, ws, rs, ps) = res["threaded"], res["sequential"]
+    assert lt == ls
+    for a, b in zip(wt, ws):
+        for (na, xa), (nb, xb) in zip(a, b):
+            assert na == nb and np.array_equal(xa, xb), na
+    assert rt == rs and len(rt) == 3
+    assert pt[0] == "selective" and sorted(pt) == sorted(ps)
+    # the min-weight thread's result is still the oracle's: pruned = int(n p) per layer
+    total = sum(int(r[7]) for r in lt["selective_pruned"])
+    p = total / sum(int(r[5]) for r in lt["selective_pruned"])
+    for (name, w), r in zip(wt[2], lt["min_pruned"]):
+        assert int((w == 0).sum()) == int(w.size * p) == int(r[7]), name

@@ -117,9 +117,9 @@ def test_degenerate_data(kind):
 
 @pytest.mark.parametrize("split", ["columns", "rows", "one_tile"])
 def test_tile_local_distributions_differ(split):
-    """Tiles whose local |c| distributions sit far from the segment's: their speculative slots
-    (the bins around each tile's local estimate of the ranks, published before barrier 0) miss
-    the rank's bin, so the select falls back to the per-bin slots behind barrier 1 -- results
+    """Tiles whose local |c| distributions sit far from the segment's: most workgroups hold no
+    key of the ranks' bin (empty slots after barrier 0) and a few hold nearly all of it, up to
+    the slot capacity (more: the digit-pass fallback over P behind two more barriers) -- results
     still equal the oracle and the multi-launch form."""
     host = G.W.synth_numpy((128, 784), 11, 0, 26)
     if split == "columns":

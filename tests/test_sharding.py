@@ -12,7 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from wavelettransforms_amd import workloads as W
-from wavelettransforms_amd.sharding import ShardPlan, prune_sharded
+from wavelettransforms_amd.sharding import REC_BYTES, REC_WORDS, ShardPlan, prune_sharded
 
 
 def test_lpt_plan_resnet18():
@@ -29,6 +29,16 @@ def test_lpt_plan_resnet18():
                 assert plan.offset[i] == o
                 o += plan.numels[i]
             assert o == plan.loads[r]
+        # the regions lie back to back, 16-byte aligned, unpadded: weights + <= 3 pad words + records
+        assert plan.base[0] == 0 and plan.total == sum(plan.size)
+        for r in range(world):
+            assert plan.base[r] % 4 == 0 and plan.rec_off[r] % 4 == 0
+            assert plan.size[r] - plan.loads[r] - len(plan.mine[r]) * REC_WORDS in range(4)
+            if r + 1 < world:
+                assert plan.base[r + 1] == plan.base[r] + plan.size[r]
+            assert plan.bytes_received(r) == 4 * (plan.total - plan.size[r])
+        if world == 8:  # every rank receives at most the whole model's weights (+ records)
+            assert max(plan.bytes_received(r) for r in range(world)) <= 4 * 11_166_912 + 20 * REC_BYTES + 8 * 12
 
 
 def _oracle_prune(wavelet, level, pct):

@@ -364,6 +364,7 @@ void inverse_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s)
 /* ---- the one-launch small path (small.hip) ---- */
 constexpr int64_t SM_POP_MAX = 1 << 20; /* population of a whole call taken by k_small */
 constexpr int SM_TILES_MAX = SM_SEG_WG_MAX; /* workgroups per tensor */
+constexpr int64_t SM_TILE_COST = 64;         /* tiling choice: LDS words a workgroup is worth */
 
 /* Tile sizes (TR x TC at level L) for one tensor: every tile's forward and inverse arena must
  * fit; among those, the least per-workgroup level-0 window plus a charge per workgroup. */
@@ -392,11 +393,7 @@ bool small_tiling(const TPlan& p, int F, int budget, int words, SmallSeg& sg) {
                         fits = sm_fwd_words(nd) <= SM_ARENA && sm_inv_words(nd) <= SM_ARENA;
                         worst = std::max<int64_t>(worst, (int64_t)ar[i].fw[0].len * ac[j].fw[0].len + nd.fkeys / 2);
                     }
-                static const int64_t tile_cost = [] { /* lab knob: LDS words a workgroup is worth */
-                    const char* e = getenv("WTP_SM_TILECOST");
-                    return e && atoi(e) >= 0 ? (int64_t)atoi(e) : (int64_t)64;
-                }();
-                const int64_t cost = worst + tile_cost * tiles;
+                const int64_t cost = worst + SM_TILE_COST * tiles;
                 if (fits && cost < best) {
                     best = cost;
                     sg.TR = TR;
@@ -417,7 +414,7 @@ bool small_tiling(const TPlan& p, int F, int budget, int words, SmallSeg& sg) {
 bool plan_small(const std::vector<TPlan>& ps, const wtp_tensor* ts, int n, void* ws, double pct, const Taps& tp,
                 uint32_t* slots, SmallTable& t) {
     if (n > SM_MAX_SEG || (tp.F & 1) || tp.F < 2 || tp.F > SM_F_MAX) return false;
-    const int cap = std::min(resident_capacity(), RES_MAX_WG);
+    const int cap = std::min(small_capacity(), RES_MAX_WG);
     int64_t tot = 0;
     for (const TPlan& p : ps) {
         if (!p.dwt || p.flat || p.L > SM_LMAX || p.H > SM_LINE_MAX || p.W > SM_LINE_MAX) return false;
@@ -429,13 +426,9 @@ bool plan_small(const std::vector<TPlan>& ps, const wtp_tensor* ts, int n, void*
     for (int i = 0; i < n; ++i) {
         const TPlan& p = ps[i];
         SmallSeg& sg = t.s[i];
-        static const int tiles_max = [] { /* lab knob: workgroups per tensor */
-            const char* e = getenv("WTP_SM_TILES");
-            return e && atoi(e) > 0 ? atoi(e) : SM_TILES_MAX;
-        }();
         /* workgroups by share of the population, at least one per image */
         if (p.B > SM_SEG_WG_MAX) return false;
-        const int budget = (int)std::max<int64_t>(p.B, std::min<int64_t>(std::min(tiles_max, SM_SEG_WG_MAX),
+        const int budget = (int)std::max<int64_t>(p.B, std::min<int64_t>(std::min(SM_TILES_MAX, SM_SEG_WG_MAX),
                                                                          (int64_t)cap * p.pop / tot));
         if (!small_tiling(p, tp.F, budget, (SM_WIN_WORDS - words) / (n - i), sg)) return false;
         /* the windows of every tile row and tile column, packed (small_geom.h computes them) */

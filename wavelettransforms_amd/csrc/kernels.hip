@@ -408,8 +408,7 @@ __device__ __forceinline__ void window_search_wave(const SegDesc& sd, const uint
 }
 
 /* -------------------------------------------------------------- k_collect --- */
-/* LAB: 0 = the production kernel; 1 = stop after the counters; 2 = stop after the bucket
- * histogram (tools/mb/lab.hip ablations).  IT float4 per thread: a sub-chunk of IT * CT * 4
+/* IT float4 per thread: a sub-chunk of IT * CT * 4
  * elements per block.  FULL: a whole 16-byte-aligned sub-chunk (unpredicated loads);
  * otherwise a ragged or unaligned one (range-checked buffer loads).
  *
@@ -418,7 +417,7 @@ __device__ __forceinline__ void window_search_wave(const SegDesc& sd, const uint
  * in the thread's own LDS column (stage[i * CT + tid], conflict-free, no scan).  A thread may
  * stage up to STG of its 4*IT keys; more sends the segment to the full-scan select. */
 constexpr int STG = 24;
-template <int CT, int IT, bool FULL, int LAB, bool WIN>
+template <int CT, int IT, bool FULL, bool WIN>
 __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __restrict__ st,
                                              uint32_t* __restrict__ cand, int64_t base, int len, bool first,
                                              uint32_t* lsub, uint32_t* lbase, uint32_t* stage,
@@ -495,11 +494,10 @@ __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __rest
         if (ovf) atomicOr(&st->overflow, 1u);
     }
     /* uniform: nothing inside the window here, or a thread overflowed (full-scan select) */
-    if (LAB == 1 || total == 0 || ovf) return;
+    if (total == 0 || ovf) return;
     WTP_CPROBE(3);
     for (uint32_t i = 0; i < cnt; ++i) atomicAdd(&lsub[(stage[i * CT + threadIdx.x] - kl - 1) >> sh], 1u);
     __syncthreads();
-    if (LAB == 2) return;
     /* reserve one contiguous run per non-empty bucket (one returning atomic per bucket, all of a
      * thread's in flight at once) */
     {
@@ -959,7 +957,7 @@ __global__ __launch_bounds__(WIN_THREADS) void k_window(SegTable t, SelHeader* _
 /* one block per sub-chunk: block b takes sub-chunk (b % SPLIT) of table block (b / SPLIT).
  * The block also clears its share of the idle SelState region (the previous group's) and the
  * zero count of its segment's result; the last block to finish flips the region parity. */
-template <int LAB, int CT, int IT, bool WIN>
+template <int CT, int IT, bool WIN>
 __global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelHeader* __restrict__ head, uint32_t* __restrict__ cand,
                                                   wtp_result* __restrict__ res) {
     constexpr int SUB = IT * CT * 4, SPLIT = CHUNK / SUB;
@@ -991,9 +989,9 @@ __global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelHeader* __restr
     if (first && threadIdx.x == 0) res[sd.res].zero_count = 0; /* k_mask_select and the inverse add */
     if (len > 0) {
         if ((sd.flags & SEG_ALIGNED) && len == SUB)
-            collect_body<CT, IT, true, LAB, WIN>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
+            collect_body<CT, IT, true, WIN>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
         else
-            collect_body<CT, IT, false, LAB, WIN>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
+            collect_body<CT, IT, false, WIN>(sd, st, cand, base, len, first, lsub, lbase, stage, wl, wred, wtot);
     }
     __syncthreads(); /* every wave has read the parity */
     /* the grid's last block flips the parity (visible to the next kernel at the boundary).  Its
@@ -2212,15 +2210,12 @@ static bool window_inline(const SegTable& t) { return collect_blocks(t) <= WINDO
 void launch_window(const SegTable& t, SelHeader* head, hipStream_t s) {
     if (!window_inline(t)) hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, s, t, head);
 }
-#ifndef WTP_COLLECT_LAB /* lab ablations only (1: stop after the counters, 2: after the bucket histogram) */
-#define WTP_COLLECT_LAB 0
-#endif
 void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s) {
     if (window_inline(t))
-        hipLaunchKernelGGL((k_collect_t<0, COLLECT_THREADS, COLLECT_IT, true>), dim3(collect_blocks(t)),
+        hipLaunchKernelGGL((k_collect_t<COLLECT_THREADS, COLLECT_IT, true>), dim3(collect_blocks(t)),
                            dim3(COLLECT_THREADS), 0, s, t, head, cand, res);
     else
-        hipLaunchKernelGGL((k_collect_t<WTP_COLLECT_LAB, COLLECT_THREADS, COLLECT_IT, false>), dim3(collect_blocks(t)),
+        hipLaunchKernelGGL((k_collect_t<COLLECT_THREADS, COLLECT_IT, false>), dim3(collect_blocks(t)),
                            dim3(COLLECT_THREADS), 0, s, t, head, cand, res);
 }
 void launch_minprune(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
@@ -2257,7 +2252,7 @@ int resident_capacity() {
     return cap > 0 ? cap : 0;
 }
 static std::atomic<uint32_t> g_res_timeout_us{RES_TIMEOUT_DEFAULT_US};
-uint32_t set_resident_timeout_us(uint32_t us) { return g_res_timeout_us.exchange(us); }
+uint32_t set_resident_timeout_us(uint32_t us) { return g_res_timeout_us.exchange(std::min(us, RES_TIMEOUT_MAX_US)); }
 static std::atomic<unsigned long long*> g_stamps{nullptr};
 void set_kernel_stamps(unsigned long long* dev) { g_stamps.store(dev); }
 uint32_t resident_timeout_us() { return g_res_timeout_us.load(std::memory_order_relaxed); }

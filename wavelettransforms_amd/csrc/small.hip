@@ -26,6 +26,8 @@
 #include "wtp_internal.h"
 #include "small_geom.h"
 
+#include <atomic>
+
 static_assert(SM_MAX_L == wtp::SM_LMAX, "level bound");
 
 #pragma clang fp contract(off)
@@ -71,11 +73,7 @@ static_assert(SM_MAX_SEG * sizeof(SmallState) <= SEG_PER_LAUNCH * sizeof(SelStat
 __device__ __forceinline__ uint32_t sm_abs_key(float x) { return __float_as_uint(x) & 0x7FFFFFFFu; }
 template <class T>
 __device__ __forceinline__ void sm_stc(T* p, T v) {
-#ifdef WTP_SM_PLAIN_P /* lab only: plain stores (NOT a valid hand-off) to time the write-through cost */
-    *p = v;
-#else
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
 }
 template <class T>
 __device__ __forceinline__ T sm_ldc(const T* p) {
@@ -488,19 +486,15 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                     K[li] = k1;
                     K[li + plane] = k2;
                     K[li + 2 * plane] = k3;
-#ifndef WTP_SM_NOHIST /* lab only: time the histogram's LDS atomics */
                     atomicAdd(&hist[k1 >> 19], 1u);
                     atomicAdd(&hist[k2 >> 19], 1u);
                     atomicAdd(&hist[k3 >> 19], 1u);
-#endif
                     mx = max(mx, max(k1, max(k2, k3)));
                     if (last) {
                         sm_stc(P + (int64_t)r * g.PC + c, aa);
                         const uint32_t k0 = sm_abs_key(aa);
                         K[li + 3 * plane] = k0;
-#ifndef WTP_SM_NOHIST
                         atomicAdd(&hist[k0 >> 19], 1u);
-#endif
                         mx = max(mx, k0);
                     }
                 }
@@ -632,26 +626,20 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
         SM_PROBE(4);
         /* every level's coefficient windows of the inverse, from P (complete since barrier 0):
          * issued now, their round trip hidden behind this barrier's wait */
-#ifdef WTP_SM_PF0 /* lab: wave 0 (the polling wave) issues none of the prefetch */
-        constexpr int PB = 64;
-#else
-        constexpr int PB = 0;
-#endif
-        constexpr int PT = SM_THREADS - PB;
         float pv[SM_PF];
 #pragma unroll
         for (int u = 0; u < SM_PF; ++u) {
-            const int e = tid - PB + u * PT;
-            pv[u] = (tid >= PB && e < nwin) ? sm_ldc(win_src(e)) : 0.0f;
+            const int e = tid + u * SM_THREADS;
+            pv[u] = e < nwin ? sm_ldc(win_src(e)) : 0.0f;
         }
         ok = sm_wait(&st->bar[1][0], a1, nwg, tmo, &s_ok);
         SM_PROBE(5);
 #pragma unroll
         for (int u = 0; u < SM_PF; ++u) {
-            const int e = tid - PB + u * PT;
-            if (tid >= PB && e < nwin) WIN[e] = pv[u];
+            const int e = tid + u * SM_THREADS;
+            if (e < nwin) WIN[e] = pv[u];
         }
-        for (int e = tid + SM_PF * PT; e < nwin; e += SM_THREADS) WIN[e] = sm_ldc(win_src(e));
+        for (int e = tid + SM_PF * SM_THREADS; e < nwin; e += SM_THREADS) WIN[e] = sm_ldc(win_src(e));
         SM_PROBE(7);
     }
     if (ok) {
@@ -805,10 +793,6 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     auto tl = [&](float c) { return (fabsf(c) < thr32) ? 0.0f : c; };
 
     /* ---------------- I: synthesis of the owned output block ---------------- */
-#ifdef WTP_SM_NOPF
-    for (int e = tid; e < nwin; e += SM_THREADS) WIN[e] = sm_ldc(win_src(e));
-    __syncthreads();
-#endif
     /* the np.where of :31 is applied as the packed coefficients are read below (tA: the cA plane
      * of level L, packed too; the synthesised ones are not thresholded) */
     int ia = 0, ilh = 0;
@@ -958,6 +942,29 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
 }
 
 /* ------------------------------------------------------------------ host --- */
+int small_capacity() {
+    static std::atomic<int> cache[16];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+    if (dev < 16) {
+        const int c = cache[dev].load(std::memory_order_relaxed);
+        if (c) return c > 0 ? c : 0;
+    }
+    int cus = 0, cap = -1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
+        const void* ks[] = {(const void*)k_small<0>, (const void*)k_small<2>, (const void*)k_small<4>,
+                            (const void*)k_small<6>, (const void*)k_small<8>, (const void*)k_small<10>,
+                            (const void*)k_small<12>, (const void*)k_small<16>, (const void*)k_small<18>};
+        cap = cus; /* one workgroup per CU, if every instance can hold one */
+        for (const void* k : ks) {
+            int per = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, SM_THREADS, 0) != hipSuccess || per < 1) cap = -1;
+        }
+    }
+    (void)hipGetLastError();
+    if (dev < 16) cache[dev].store(cap, std::memory_order_relaxed);
+    return cap > 0 ? cap : 0;
+}
 void launch_small(const SmallTable& t0, SelHeader* head, wtp_result* res, hipStream_t s) {
     SmallTable t = t0;
     t.timeout = resident_timeout_us() * 100u; /* 100 MHz wall clock */

@@ -204,7 +204,10 @@ constexpr int RES_WG_WORDS = RES_SLOT_WORDS;        /* one workgroup's slot in t
 constexpr int RES_SEL_MAX = 1024;                   /* keys the one-wave select takes (more: full scan) */
 constexpr uint32_t RES_TIMEOUT_DEFAULT_US = 200000; /* a wait this long means the grid is not co-resident */
 int resident_capacity();
-uint32_t set_resident_timeout_us(uint32_t us); /* every k_resident wait's bound; returns the previous one */
+/* every resident wait's bound (k_resident, k_small), clamped to RES_TIMEOUT_MAX_US so that the
+ * bound in 100 MHz ticks fits 32 bits; returns the previous one */
+constexpr uint32_t RES_TIMEOUT_MAX_US = 40000000u;
+uint32_t set_resident_timeout_us(uint32_t us);
 void set_kernel_stamps(unsigned long long* dev); /* k_resident / k_small launch span stamps (measurement) */
 uint32_t resident_timeout_us();
 unsigned long long* kernel_stamps();
@@ -255,6 +258,9 @@ struct SmallTable {
 };
 static_assert(sizeof(SmallTable) <= 4096, "k_small's kernel argument");
 void launch_small(const SmallTable& t, SelHeader* head, wtp_result* res, hipStream_t s);
+/* workgroups k_small may launch at once on the current device (one per CU, every F instance
+ * checked by the occupancy query); 0: never used */
+int small_capacity();
 
 /* min-weight pruning after window + collect: mp = 16 B per tensor, tiecnt = one u32 per
  * streaming block */

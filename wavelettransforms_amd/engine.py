@@ -26,7 +26,9 @@ def wavelet_id(name):
 def workspace(device, nbytes, stream=None):
     """Grow-only, zero-initialised workspace per (device, stream): the selection, barrier and
     parity state of a call live in it, so calls on distinct streams need distinct workspaces
-    (include/wtprune.h).  The library keeps it clean between calls on its stream."""
+    (include/wtprune.h).  The library keeps it clean between calls on its stream.  Each stream
+    ever used keeps its workspace (at the largest size it needed: a cfg5-sized call holds the
+    packed coefficients of its images) until release_workspaces() drops it."""
     device = torch.device(device)
     if device.index is None:
         device = torch.device(device.type, torch.cuda.current_device())
@@ -40,6 +42,18 @@ def workspace(device, nbytes, stream=None):
             ws = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         _workspaces[key] = ws
     return ws
+
+
+def release_workspaces(device=None, stream=None):
+    """Drop the cached workspaces (all, one device's, or one (device, stream)'s): their memory goes
+    back to torch's caching allocator.  Call it after the stream's work has been waited for or
+    when retiring a stream whose handle may be recycled; the next call allocates a zeroed one."""
+    for key in list(_workspaces):
+        if device is not None and key[0] != torch.device(device).index:
+            continue
+        if stream is not None and key[1] != stream.cuda_stream:
+            continue
+        del _workspaces[key]
 
 
 def _results(n, device, stream):
