@@ -245,3 +245,45 @@ def test_outs_validated(eng):
         eng.launch([x], "bior3.3", 5, 50.0, outs=[torch.empty(10, device="cuda")])
     with pytest.raises(TypeError):
         eng.launch([x], "bior3.3", 5, 50.0, outs=[torch.empty(64, 64, 3, 3, device="cuda", dtype=torch.float64)])
+
+
+def _halves_input(n, seed, scale_b):
+    """The second half of every 2048-element run (the float4 slots of waves 4-7 of a resident
+    workgroup) drawn from a distribution scaled by scale_b: the chunk's waves see different local
+    distributions."""
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal(n) * 0.05).astype(np.float32)
+    x[(np.arange(n) % 2048) >= 1024] *= np.float32(scale_b)
+    return x
+
+
+@pytest.mark.parametrize("pct", [10.0, 50.0, 90.0])
+@pytest.mark.parametrize("in_place", [False, True], ids=["out_of_place", "in_place"])
+def test_structured_halves(eng, mode, pct, in_place):
+    n = 600_000
+    x = _halves_input(n, 5, 1.06)
+    ref, rr = O.prune_tensor(x.reshape(600, 1000), "bior3.3", 0, pct)
+    xt = _dev(x).reshape(600, 1000)
+    outs, (r,) = eng.prune([xt], "bior3.3", 0, pct, outs=[xt] if in_place else None)
+    assert r["path"] in (1, 2), r["path"]
+    _same(outs[0].cpu().numpy(), ref, r, rr)
+
+
+def test_nan_and_inf_in_either_half(eng, mode):
+    """NaN / inf in the first or the second half of a 2048-element run (loaded by different waves
+    of a resident workgroup), and past the first chunk."""
+    rng = np.random.default_rng(9)
+    base = (rng.standard_normal(200_000) * 0.05).astype(np.float32)
+    cases = []
+    for pos in (1500, 50_000 + 2047, 700):  # B, B, A half
+        a = base.copy()
+        a[pos] = np.nan
+        b = base.copy()
+        b[pos] = -np.inf
+        cases += [a, b]
+    outs, res = eng.prune([_dev(c) for c in cases], "db8", 5, 61.8, carry_level=False)
+    for xin, o, r in zip(cases, outs, res):
+        ref, rr = O.prune_tensor(xin.copy(), "db8", 5, 61.8)
+        assert np.array_equal(o.cpu().numpy(), ref, equal_nan=True)
+        assert r["zero_count"] == rr["zero_count"]
+        assert G.f64_bits_equal(r["thr64"], rr["thr64"]) or (np.isnan(r["thr64"]) and np.isnan(rr["thr64"]))

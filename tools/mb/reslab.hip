@@ -16,6 +16,7 @@ __device__ unsigned long long g_sprobe[256][16];
 #endif
 #include "../../wavelettransforms_amd/csrc/kernels.hip"
 #include "../../wavelettransforms_amd/csrc/filterbank.hip"
+#include "../../wavelettransforms_amd/csrc/small.hip"
 #include "../../wavelettransforms_amd/csrc/api.hip"
 #include <cstdio>
 #include <vector>

@@ -35,20 +35,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #endif
 
 /* waves per SIMD the filter-bank kernels are register-budgeted for (db8: 5 needs <= 96 VGPRs) */
-#ifndef WTP_FB_FWD_WPE
 #define WTP_FB_FWD_WPE __attribute__((amdgpu_waves_per_eu(5)))
-#endif
-#ifndef WTP_FB_INV_WPE
 #define WTP_FB_INV_WPE __attribute__((amdgpu_waves_per_eu(5)))
-#endif
 
 constexpr int FB_THREADS = 256;
 constexpr int FR = 16, FC = 64;  /* forward output tile (per subband) */
 constexpr int IR = 64, IC = 64;  /* inverse output tile */
-#ifndef WTP_INV_RG
-#define WTP_INV_RG 2
-#endif
-constexpr int INV_RG = WTP_INV_RG; /* synthesis row-pass rows interleaved per wave */
+constexpr int INV_RG = 2; /* synthesis row-pass rows interleaved per wave */
 constexpr int FB_MAX_LDS = 64 * 1024;
 
 /* XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (blocks b and b+8

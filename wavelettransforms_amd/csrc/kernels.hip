@@ -205,26 +205,8 @@ __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, i
 #ifndef WTP_WPROBE
 #define WTP_WPROBE(i)
 #endif
-#ifndef WTP_RES_CNT /* k_resident's below / == kl counts: 1 ballot popcounts (scalar unit), 0 per-lane */
-#define WTP_RES_CNT 0
-#endif
-#ifndef WTP_RES_FLIP_SHARD /* k_resident's parity flip: 1 sharded counters off the polling lane, 0 one counter */
-#define WTP_RES_FLIP_SHARD 1
-#endif
-#ifndef WTP_RES_SPEC /* k_resident: speculative stores of the decided keys during the second barrier */
-#define WTP_RES_SPEC 0
-#endif
-#ifndef WTP_RES_NTST /* k_resident's output stores: 1 nontemporal (tools/mb/reslab.hip A/B) */
-#define WTP_RES_NTST 1
-#endif
-#ifndef WTP_RES_FSEL /* k_resident's final select: 1 one-wave radix selects, 0 the block radix select */
-#define WTP_RES_FSEL 0
-#endif
-#ifndef WTP_RES_P0 /* k_resident's load order (tools/mb/reslab.hip A/B) */
-#define WTP_RES_P0 1
-#endif
-#ifndef WTP_RES_ABL /* tools/mb/reslab.hip ablations: bit 0 window, 1 count, 2 bucket scatter, 3 select, 4 barrier */
-#define WTP_RES_ABL 0
+#ifndef WTP_GPROBE /* a probe taken by lane 0 of the executing wave */
+#define WTP_GPROBE(i)
 #endif
 
 /* ------------------------------------------------------------ the window --- */
@@ -1200,49 +1182,6 @@ __device__ __forceinline__ void window_search_flat(const SegDesc& sd, const uint
 }
 
 
-/* Rank r (0-based, ascending) among the m keys stage[0..m), all in [lo, hi]: ONE wave, an MSB-first
- * radix select in 8-bit digits below the common prefix of lo and hi over a private 256-bin LDS
- * histogram h.  A wave's LDS instructions complete in order, so no barrier separates the clear,
- * the adds and the reads -- but the compiler must not forward a lane's own clear to its read of
- * bins other lanes added to (the asm memory clobbers).  Every lane of the wave must be active. */
-__device__ __forceinline__ uint32_t wave_radix_select(const uint32_t* stage, int m, int r, uint32_t lo, uint32_t hi,
-                                                      uint32_t* h) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t diff = lo ^ hi;
-    int top = diff ? 31 - __clz(diff) : -1; /* highest unknown bit */
-    uint32_t mask = top >= 31 ? 0u : ~((2u << top) - 1u);
-    uint32_t prefix = lo & mask;
-    while (top >= 0) {
-        const int width = top + 1 < 8 ? top + 1 : 8;
-        const int shift = top + 1 - width;
-        const uint32_t dm = (1u << width) - 1u;
-        reinterpret_cast<uint4*>(h)[lane] = make_uint4(0u, 0u, 0u, 0u);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* other lanes' bins: no store forwarding */
-        for (int i = lane; i < m; i += 64) {
-            const uint32_t k = stage[i];
-            if ((k & mask) == prefix) atomicAdd(&h[(k >> shift) & dm], 1u);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the adds of every lane land before the reads */
-        const uint4 c = reinterpret_cast<const uint4*>(h)[lane]; /* bins 4 lane .. 4 lane + 3 */
-        const uint32_t sum = c.x + c.y + c.z + c.w;
-        const uint32_t incl = wave_scan_u32(sum);
-        const uint32_t excl = incl - sum;
-        const uint64_t hit = __ballot((uint32_t)r >= excl && (uint32_t)r < incl);
-        const int L = hit ? __ffsll((unsigned long long)hit) - 1 : 63; /* r < m: always hit */
-        uint32_t d = 4u * (uint32_t)lane, below = excl;
-        if ((uint32_t)r >= below + c.x) { below += c.x; ++d;
-            if ((uint32_t)r >= below + c.y) { below += c.y; ++d;
-                if ((uint32_t)r >= below + c.z) { below += c.z; ++d; } } }
-        d = (uint32_t)__builtin_amdgcn_readlane((int)d, L);
-        below = (uint32_t)__builtin_amdgcn_readlane((int)below, L);
-        prefix |= d << shift;
-        mask |= dm << shift;
-        r -= (int)below;
-        top = shift - 1;
-    }
-    return prefix;
-} /* a segment barrier counter whose wait timed out */
-
 __device__ __forceinline__ uint64_t wall_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
 /* Wait until the segment barrier counter reaches `want` arrivals (one lane polls with sc1 loads,
@@ -1291,6 +1230,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     const uint64_t tmo = t.res_timeout;
     WTP_RPROBE(0);
     __shared__ uint32_t s_win[3];
+    __shared__ uint32_t s_sync; /* the sampling waves' LDS meeting counter */
     float4 v[IT];
     /* ---- P0: the sample waves' loads go out before any chunk load of the workgroup (the barrier
      * below orders them), then every wave issues its chunk; the sample arrives first (a wave's
@@ -1308,57 +1248,50 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 const int i = j * (64 * RES_SW) + tid;
                 const int64_t pos = exact ? min((int64_t)i, n - 1)
                                           : (int64_t)((double)(i / SAMPLE_GROUP) * step) + (i % SAMPLE_GROUP);
-                ks[j] = abs_key(sd.data[pos]);
+                ks[j] = __float_as_uint(sd.data[pos]); /* raw bits: |x| at the histogram */
             }
         }
         for (int j = tid; j < RES_HBINS; j += CT) raw[j] = 0u;
         for (int j = tid; j < RES_NSUB; j += CT) lsub[j] = 0u;
+        if (tid == 0) s_sync = 0u;
         if (first && tid == 0) { /* memory-side words: later adds come from other workgroups */
             stc(reinterpret_cast<unsigned long long*>(&res[sd.res].zero_count), 0ull);
             stc(&res[sd.res].path, 0);
         }
-        __syncthreads();
+        __syncthreads(); /* the sample's loads are out before any chunk load of the workgroup */
         WTP_RPROBE(8);
-#if WTP_RES_P0 == 1
-        /* the non-sampling waves stream at once; the sampling waves histogram their sample first
-         * (it comes back ahead of the flood) and issue their chunk after */
-        if (wv >= RES_SW) {
-            if (FULL) load_chunk<IT, CT>(sd.data + base, v);
-            else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
-        } else {
+        /* the sampling waves histogram their sample (it comes back ahead of the flood) and wave 0
+         * searches the window; the other waves go straight to the loads.  The chunk is loaded at
+         * ONE program point by every wave: a single definition of v[], so the compiler keeps the
+         * loads' destination registers and nothing waits for the data before it is counted; the
+         * sample's |x| is taken here, behind the barrier, by an AND the compiler cannot fold back
+         * into the loads' block (it would make the sampling waves wait for the sample before the
+         * barrier) */
+        if (wv < RES_SW) {
 #pragma unroll
             for (int j = 0; j < RES_SPL; ++j)
-                if (j * (64 * RES_SW) + tid < m) atomicAdd(&raw[key_bin(ks[j])], 1u);
+                if (j * (64 * RES_SW) + tid < m) {
+                    uint32_t k;
+                    asm volatile("v_and_b32 %0, 0x7fffffff, %1" : "=v"(k) : "v"(ks[j]));
+                    atomicAdd(&raw[key_bin(k)], 1u);
+                }
+            /* the sampling waves meet on an LDS counter (the others do not wait for them) */
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) atomicAdd(&s_sync, 1u);
+            if (wv == 0) {
+                while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_sync, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_WORKGROUP)) < (uint32_t)RES_SW)
+                    __builtin_amdgcn_s_sleep(1);
+                asm volatile("" ::: "memory");
+                uint32_t wkl, wkh, wsh;
+                window_search_flat(sd, raw, m, exact, &wkl, &wkh, &wsh, RES_SIGMA_X100 * 0.01, 8.0);
+                if (lane == 0) { s_win[0] = wkl; s_win[1] = wkh; s_win[2] = wsh; }
+                WTP_RPROBE(1);
+            }
         }
-        __syncthreads();
-        if (wv == 0) {
-            uint32_t wkl, wkh, wsh;
-            window_search_flat(sd, raw, m, exact, &wkl, &wkh, &wsh, t.pad[1] * 0.01, 8.0);
-            if (lane == 0) { s_win[0] = wkl; s_win[1] = wkh; s_win[2] = wsh; }
-            WTP_RPROBE(1);
-        }
-        if (wv < RES_SW) {
-            if (FULL) load_chunk<IT, CT>(sd.data + base, v);
-            else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
-        }
-        WTP_RPROBE(10);
-#else
         if (FULL) load_chunk<IT, CT>(sd.data + base, v);
         else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
         WTP_RPROBE(10);
-        if (wv < RES_SW) {
-#pragma unroll
-            for (int j = 0; j < RES_SPL; ++j)
-                if (j * (64 * RES_SW) + tid < m) atomicAdd(&raw[key_bin(ks[j])], 1u);
-        }
-        __syncthreads();
-        if (wv == 0) {
-            uint32_t wkl, wkh, wsh;
-            window_search_flat(sd, raw, m, exact, &wkl, &wkh, &wsh, t.pad[1] * 0.01, 8.0);
-            if (lane == 0) { s_win[0] = wkl; s_win[1] = wkh; s_win[2] = wsh; }
-            WTP_RPROBE(1);
-        }
-#endif
     }
     __syncthreads();
     const uint32_t kl = s_win[0], kh = s_win[1];
@@ -1446,7 +1379,6 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
      * lane 0 of wave 1, off the polling lane's path, through per-shard counters (blockIdx % 8;
      * the last arriver of a shard adds to the top counter) so no address queues more than
      * ~gridDim / 8 returning adds */
-#if WTP_RES_FLIP_SHARD
     if (tid == 64) {
         const uint32_t sh8 = blockIdx.x & (NSHARD - 1);
         const uint32_t nsh = (gridDim.x - sh8 + NSHARD - 1) / NSHARD;
@@ -1454,9 +1386,6 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         if (atomicAdd(&bar->arrive[sh8][0], 1u) == nsh - 1u && atomicAdd(&bar->arrive[0][16], 1u) == nact - 1u)
             stc(&head->parity, q ^ 1u);
     }
-#else
-    if (tid == 0 && atomicAdd(&bar->arrive[0][0], 1u) == gridDim.x - 1u) stc(&head->parity, q ^ 1u);
-#endif
     WTP_RPROBE(4);
     if (!res_wait(b1, nwg, tmo)) {
         if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
@@ -1536,8 +1465,6 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     __syncthreads();
     WTP_PROBE(2);
     bool full = ca == 0 || cb == 0 || s_ovf != 0;
-    bool specd = false;   /* this workgroup's chunk was stored speculatively */
-    uint32_t spec_lo = 0; /* keys below it were stored pruned, the rest unpruned */
     int path = MODE_WINDOW;
     uint32_t ka = kl, kb = kl;
     uint32_t before = 0;
@@ -1574,25 +1501,6 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             /* ---- segment barrier 2: every slot of the segment is written */
             res_arrive(b2);
             WTP_PROBE(3);
-#if WTP_RES_SPEC
-            /* speculative stores while the segment's slots come in (out of place only: a segment
-             * that still falls back to the full scan re-reads its intact input; never with inf /
-             * NaN keys): every key outside buckets ba..bb is decided -- below them pruned, above
-             * them kept -- and the undecided ones are written unpruned and fixed after the select */
-            if (FULL && sd.out != sd.data && mk < 0x7F800000u) {
-                const uint32_t ulo = (uint32_t)((uint64_t)kl + ((uint64_t)ba << sh));
-                float4* q4 = reinterpret_cast<float4*>(sd.out + base);
-                typedef float f4v __attribute__((ext_vector_type(4)));
-                auto g = [&](float xv) { return abs_key(xv) < ulo ? 0.0f : xv; };
-#pragma unroll
-                for (int it = 0; it < IT; ++it) {
-                    const f4v yv = {g(v[it].x), g(v[it].y), g(v[it].z), g(v[it].w)};
-                    __builtin_nontemporal_store(yv, reinterpret_cast<f4v*>(q4 + it * CT + tid));
-                }
-                specd = true;
-                spec_lo = ulo;
-            }
-#endif
             if (!res_wait(b2, nwg, tmo)) {
                 if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
                 return;
@@ -1651,22 +1559,8 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 const uint32_t lo = (uint32_t)((uint64_t)kl + ((uint64_t)ba << sh));
                 const uint32_t hi = (uint32_t)min((uint64_t)kh, (uint64_t)kl + ((uint64_t)(bb + 1) << sh) - 1);
                 uint32_t xa = kl, xb = kl;
-#if WTP_RES_FSEL == 0
                 select_in_range<CT>([&](int64_t i) { return stage[i]; }, [](uint32_t) { return true; }, (int64_t)m,
                                     lo, hi, ja - (int64_t)before, jb - (int64_t)before, ca == 2, cb == 2, &xa, &xb);
-#else
-                { /* wave 0 takes r0, wave 1 takes r1: one-wave radix selects over private histograms */
-                    __shared__ uint32_t s_x[2];
-                    if (wv < 2 && (wv == 0 ? ca : cb) == 2) {
-                        const int r = (int)((wv == 0 ? ja : jb) - (int64_t)before);
-                        const uint32_t k = wave_radix_select(stage, m, r, lo, hi, raw + RES_SEL_MAX + 256 * wv);
-                        if (lane == 0) s_x[wv] = k;
-                    }
-                    __syncthreads();
-                    xa = s_x[0];
-                    xb = s_x[1];
-                }
-#endif
                 ka = ca == 2 ? xa : kl;
                 kb = cb == 2 ? xb : kl;
                 path = MODE_CAND;
@@ -1733,30 +1627,15 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     /* ---- P3: out = where(|x| < thr, 0, x) from registers (a NaN threshold prunes nothing) */
     float* qo = sd.out + base;
     auto fin = [&](float xv) { return (fabsf(xv) < thr) ? 0.0f : xv; };
-    if (specd && path == MODE_CAND && !nan) {
-        /* only the keys the speculative store left unpruned that the threshold prunes: one
-         * dword each (a few per workgroup) */
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float xv = f4_get(v[it], c);
-                if (abs_key(xv) >= spec_lo && fabsf(xv) < thr) qo[4 * (it * CT + tid) + c] = 0.0f;
-            }
-        }
-    } else if (FULL) {
+    if (FULL) {
         float4* q4 = reinterpret_cast<float4*>(qo);
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
             float4 y;
             y.x = fin(v[it].x); y.y = fin(v[it].y); y.z = fin(v[it].z); y.w = fin(v[it].w);
-#if WTP_RES_NTST
             typedef float f4v __attribute__((ext_vector_type(4)));
             const f4v yv = {y.x, y.y, y.z, y.w};
             __builtin_nontemporal_store(yv, reinterpret_cast<f4v*>(q4 + it * CT + tid));
-#else
-            q4[it * CT + tid] = y;
-#endif
         }
     } else {
         const __amdgpu_buffer_rsrc_t rr = ragged_rsrc(qo, len);
@@ -2259,9 +2138,7 @@ uint32_t resident_timeout_us() { return g_res_timeout_us.load(std::memory_order_
 unsigned long long* kernel_stamps() { return g_stamps.load(std::memory_order_relaxed); }
 void launch_resident(const SegTable& t0, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
                      hipStream_t s) {
-    static const int sig = [] { const char* e = getenv("WTP_RES_SIGMA"); return e && atoi(e) > 0 ? atoi(e) : RES_SIGMA_X100; }();
     SegTable t = t0;
-    t.pad[1] = sig; /* window margin: sig/100 binomial sigma + 8 sample ranks */
     t.res_timeout = g_res_timeout_us.load(std::memory_order_relaxed) * 100u; /* 100 MHz wall clock */
     t.stamps = g_stamps.load(std::memory_order_relaxed);
     hipLaunchKernelGGL(k_resident, dim3(t.nblk), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);

@@ -44,10 +44,7 @@ namespace wtp {
 #define SM_PROBE(i)
 #endif
 
-#ifndef WTP_SM_THREADS
-#define WTP_SM_THREADS 1024
-#endif
-constexpr int SM_THREADS = WTP_SM_THREADS;
+constexpr int SM_THREADS = 1024;
 static_assert(SM_THREADS >= 256 && SM_THREADS <= 1024 && (SM_THREADS & (SM_THREADS - 1)) == 0, "k_small block");
 constexpr int SM_NW = SM_THREADS / 64;
 constexpr int SM_PF = 8; /* inverse-window words per thread prefetched in registers */

@@ -22,13 +22,10 @@ namespace wtp {
  * ranks and resolves them exactly, or by a full radix select over the segment if the window
  * missed. */
 constexpr int M_SAMPLE = 4096;      /* k_resident: every workgroup draws it before its chunk    */
-#ifndef WTP_SAMPLE_WIN
-#define WTP_SAMPLE_WIN 65536
-#endif
 /* k_window (three-launch form): one block per segment, 64 keys a thread in passes of 16; on cfg5
  * 65536 keys (window ~2.4 % of the segment) beat 16384 (~5 %: k_collect +55 us per 24-segment
  * launch) and 262144 (~1.2 %: k_window +47 us for 10 us less k_collect) */
-constexpr int M_SAMPLE_WIN = WTP_SAMPLE_WIN;
+constexpr int M_SAMPLE_WIN = 65536;
 constexpr int SAMPLE_GROUP = 16;   /* contiguous keys per sample group */
 constexpr int NSUB_MAX = 1024;     /* buckets over (kl, kh]: 64..1024 per segment (SegDesc) */
 constexpr int RES_NSUB_LOG2 = 10;  /* k_resident: 1024 buckets over (kl, kh] (4096 measured slower: 8 KB more reads per workgroup) */
@@ -177,16 +174,10 @@ void launch_mask_inplace(const SegTable& t, const wtp_result* res, const float* 
 constexpr int RES_THREADS = 512;
 constexpr int RES_IT = 24;                          /* float4 per thread held in VGPRs */
 constexpr int RES_CHUNK = RES_THREADS * RES_IT * 4; /* 49152 elements per workgroup   */
-#ifndef WTP_RES_MS
-#define WTP_RES_MS 4096
-#endif
-#ifndef WTP_RES_SW
-#define WTP_RES_SW 4
-#endif
 /* k_resident's window sample: RES_MS keys per segment, loaded by the first RES_SW waves of every
  * workgroup (RES_SPL per lane) ahead of the chunk's loads */
-constexpr int RES_MS = WTP_RES_MS;
-constexpr int RES_SW = WTP_RES_SW;
+constexpr int RES_MS = 4096;
+constexpr int RES_SW = 4;
 constexpr int RES_SPL = RES_MS / (64 * RES_SW);
 /* a wave may have at most 63 vector-memory instructions outstanding: the sample's loads and
  * the chunk's must all be in flight together */
