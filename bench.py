@@ -36,7 +36,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VALU_NOFMA_TFLOPS = 78.6   # FP32 vector peak without FMA contraction
+# FP32 vector rate without FMA contraction, mul + add counted as two flops: MEASURED on MI355X with
+# independent v_pk_mul_f32 / v_pk_add_f32 chains at >= 2 waves per SIMD (tools/mb/pkrate.hip,
+# profiles/r03_valu_nofma_rate.txt: 128 TF/s packed, 120 TF/s scalar); SURVEY.md 8(d)'s 78.6 was
+# an estimate (half the FMA spec)
+VALU_NOFMA_TFLOPS = 128.0
 METRIC = "weight-coeffs/s for L5 bior3.3 DWT+thresh+IDWT; achieved HBM GB/s vs peak"
 STAGES = ["forward_dwt", "k_window", "k_collect", "k_mask_select", "inverse_dwt"]
 KERNEL_OF_STAGE = {"k_window": "k_window", "k_collect": "k_collect_t", "k_mask_select": "k_mask_select",
@@ -155,6 +159,29 @@ def child_steps(args):
     K = max(args.steps, 200)
     G = max(1, min(args.graph_steps, K))
     return args.warmup + K + (0 if args.no_graph else 1 + 2 * G)
+
+
+def dwt_stage_work(shapes_levels, F):
+    """Per step, over the tensors' (shape, effective level) pairs: the bytes each tiled filter-bank
+    stage moves at its minimum -- forward level k reads its R_{k-1} x C_{k-1} input and writes four
+    R_k x C_k subbands; inverse level k reads four subbands and writes its 2R_k x 2C_k output (the
+    last one cropped to H x W) -- and the flops (no FMA) each stage computes: 8 F R_k C_k MACs per
+    level and batch item, forward and inverse alike (pywt periodization: N_k = ceil(N_{k-1} / 2))."""
+    fwd = inv = flops = 0
+    for shape, L in shapes_levels:
+        if L <= 0 or len(shape) < 2:
+            continue
+        H, W = int(shape[-2]), int(shape[-1])
+        B = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+        R, C = [H], [W]
+        for _ in range(L):
+            R.append((R[-1] + 1) // 2)
+            C.append((C[-1] + 1) // 2)
+        for k in range(1, L + 1):
+            fwd += 4 * B * (R[k - 1] * C[k - 1] + 4 * R[k] * C[k])
+            inv += 4 * B * (4 * R[k] * C[k] + (H * W if k == 1 else 4 * R[k] * C[k]))
+            flops += 2 * 8 * F * R[k] * C[k] * B  # per stage
+    return {"forward_dwt": fwd, "inverse_dwt": inv, "flops_per_stage": flops}
 
 
 def cpu_model():
@@ -280,6 +307,16 @@ def main():
     # the whole call as one k_small launch (csrc/small.hip): small 2-D calls, e.g. cfg3
     small = bool(recs) and not sharded and all(r["path"] == engine.MODE_SMALL for r in recs)
 
+    # WTP_CRASH_DIAG=<dir>: Python-level fault handler into <dir>/faulthandler.txt and a snapshot
+    # of this process's memory map in <dir>/maps.txt taken just before the graph is captured, so
+    # the native frames of a crash inside a graph replay can be mapped to their libraries
+    diag = os.environ.get("WTP_CRASH_DIAG")
+    if diag:
+        import faulthandler
+        os.makedirs(diag, exist_ok=True)
+        _fh = open(os.path.join(diag, "faulthandler.txt"), "w")
+        faulthandler.enable(file=_fh, all_threads=True)
+
     # ------------------------------------------------- hipGraph (single-process configs)
     G = max(1, min(args.graph_steps, args.steps))
     graph = None
@@ -293,6 +330,9 @@ def main():
         with torch.cuda.graph(graph):
             for _ in range(G):
                 step()
+        if diag:
+            with open("/proc/self/maps") as fi, open(os.path.join(diag, "maps.txt"), "w") as fo:
+                fo.write(fi.read())
         for _ in range(2):
             graph.replay()
         torch.cuda.synchronize()
@@ -383,6 +423,7 @@ def main():
         return (h[:, 1] - h[:, 0]).astype(np.float64) * 0.01  # 100 MHz ticks -> us
 
     stage_us, dom, dom_us, dom_bytes, dom_launches, timing_src = {}, None, None, 0, 1, None
+    work = None
     if (resident or small) and xs:
         # one launch per step: its algorithmic bytes are every weight read once and written once
         spans = stamp_spans(args.stamp_reps)
@@ -411,9 +452,14 @@ def main():
         finally:
             L.wtp_set_stage_events(None, 0)
 
+        work = None if args.flatten else dwt_stage_work(
+            [(tuple(x.shape), r["eff_level"]) for x, r in zip(xs, recs)], int(L.wtp_dec_len(engine.wavelet_id(wavelet))))
+
         def sbytes(st):
             if st in DWT_STAGES and not has_dwt:
                 return 0
+            if st in DWT_STAGES and work is not None:
+                return work[st]  # the stage kernels' own inputs and outputs, level by level
             return {"forward_dwt": 4 * n_w + 4 * pop, "k_window": 0, "k_collect": 4 * pop,
                     "k_mask_select": 8 * n_w if pop == n_w else 0, "inverse_dwt": 4 * pop + 4 * n_w}[st]
         ran = [st for st in STAGES if not (st in DWT_STAGES and not has_dwt)]
@@ -551,7 +597,14 @@ def main():
                 "traffic": None if traffic is None else traffic * dom_launches,
                 "traffic_source": traffic_src and ("committed rocprofv3 --pmc summary %s (2 x FETCH_SIZE + "
                                                    "WRITE_SIZE per launch), not measured in this run" % traffic_src),
-                "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_us": dom_us, "timing": timing_src,
+                "algorithmic_bytes_per_step": dom_bytes,
+                "algorithmic_bytes_per_launch": dom_bytes / max(dom_launches, 1),
+                "bytes_basis": ("every weight read once and written once (8 B per weight)" if dom in ("k_resident", "k_small")
+                                else "the stage kernels' own inputs and outputs, level by level (tools: dwt_stage_work)"
+                                if dom in DWT_STAGES and work is not None else "stage inputs and outputs"),
+                "valu_frac": (work["flops_per_stage"] / (dom_us * 1e-6) / (VALU_NOFMA_TFLOPS * 1e12)
+                              if dom in DWT_STAGES and work is not None else None),
+                "avg_launch_us": dom_us, "timing": timing_src,
                 "avg_launch_us_stamps": stamps_us, "pmc_source_tag": traffic_tag},
             "stage_us": stage_us,
             "cpu_baseline": cpu,
@@ -565,8 +618,10 @@ def main():
             flops = DB8_L5_FLOP_PER_ELEM * n_model
             line["valu_roof"] = {"flop_per_elem": DB8_L5_FLOP_PER_ELEM, "peak_tflops": VALU_NOFMA_TFLOPS,
                                  "floor_ms": flops / (VALU_NOFMA_TFLOPS * 1e12) * 1e3 / world,
-                                 "frac": flops / (T / K) / (VALU_NOFMA_TFLOPS * 1e12) / world,
-                                 "note": "pipeline vs the no-FMA FP32 VALU roof (bit-exactness forbids contraction)"}
+                                 "frac": flops / (ms_per_step * 1e-3) / (VALU_NOFMA_TFLOPS * 1e12) / world,
+                                 "note": "whole pipeline vs the no-FMA FP32 VALU rate measured on MI355X "
+                                         "(bit-exactness forbids contraction); the dominant kernel's own "
+                                         "fraction is roofline.valu_frac"}
         if cold:
             line["cold_mall"] = cold
         if multi:

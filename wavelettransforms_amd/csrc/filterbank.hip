@@ -22,6 +22,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
+#include <vector>
 
 #pragma clang fp contract(off)
 
@@ -43,6 +45,11 @@ constexpr int FR = 16, FC = 64;  /* forward output tile (per subband) */
 constexpr int IR = 64, IC = 64;  /* inverse output tile */
 constexpr int INV_RG = 2; /* synthesis row-pass rows interleaved per wave */
 constexpr int FB_MAX_LDS = 64 * 1024;
+/* the forward input tile in LDS (specialised filters): row pitch FWD_TP floats, the tile's first
+ * column at FWD_S0 -- so that its column 0 - FWD_S0 is 16-byte aligned in the image (a tile's
+ * first input column is 2 FC tc - F/2 + 1) and interior rows load as whole float4s */
+template <int FT> constexpr int FWD_S0 = ((1 - FT / 2) % 4 + 4) % 4;
+template <int FT> constexpr int FWD_TP = (FWD_S0<FT> + 2 * FC + FT - 2 + 3) / 4 * 4;
 
 /* XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (blocks b and b+8
  * share one L2), so tile t = xcd * per + b / 8 gives each XCD a contiguous run of tiles and the
@@ -52,13 +59,6 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
     const int per = (n + 7) / 8, x = b & 7, k = b >> 3;
     const int full = n - 8 * (per - 1); /* XCDs that get `per` tiles; the rest get per - 1 */
     return x < full ? x * per + k : full * per + (x - full) * (per - 1) + k;
-}
-
-__device__ __forceinline__ int find_item(const int* blk_begin, int b) {
-    int i = 0; /* blk_begin[0] == 0 */
-#pragma unroll
-    for (int j = 1; j < FB_GROUP; ++j) i += b >= blk_begin[j];
-    return i;
 }
 
 __device__ __forceinline__ int ext_idx(int t, int N) { /* wt_ext_index in 32 bits */
@@ -260,17 +260,25 @@ struct FwdArgs {
     int PC, offR, offC;  /* level-k detail origin in the packed image */
     float* anext;        /* (B, Ro, Co) next-level approximation; unused when last */
     int last, tilesC, tilesR;
+    int al16;            /* in is 16-byte aligned and C % 4 == 0: interior tiles load float4 rows */
 };
 
-/* one launch covers the same level of up to FB_GROUP images (same filter): a block finds its
- * image by one scalar sweep of blk_begin, as k_collect finds its segment */
+/* One launch covers the same level of up to FB_UNI items of the SAME geometry (same filter; the
+ * cfg5 blocks of a call, the batch of one tensor): the geometry once, the pointers per item, and
+ * a block's item is its tile / tiles-per-item.  The specialised kernels take their taps as a
+ * SmallTaps (F <= 20): the whole argument stays near 2 KB. */
+constexpr int FB_UNI = 64;
 struct FwdGroup {
-    int blk_begin[FB_GROUP]; /* INT32_MAX past n */
-    FwdArgs it[FB_GROUP];
+    FwdArgs geo;            /* the items' geometry; its pointers are unused */
+    int n, tiles;           /* items; tiles per item */
+    const float* in[FB_UNI];
+    float* anext[FB_UNI];
+    float* P[FB_UNI];
 };
+template <int FT> using TapsT = typename std::conditional<FT == 0, Taps, SmallTaps>::type;
 
 template <int FT>
-__global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGroup g, Taps tp) {
+__global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGroup g, TapsT<FT> tp) {
     extern __shared__ float lds[];
     const int F = FT ? FT : tp.F;
     const int NR = 2 * FR + F - 2, NC = 2 * FC + F - 2;
@@ -282,9 +290,12 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
     const int HALF = (NC + 1) / 2;
     auto lhi = [&](int o, int cc) { return o * NC + (cc & 1) * HALF + (cc >> 1); };
     const int gt = xcd_tile(blockIdx.x, gridDim.x);
-    const int item = find_item(g.blk_begin, gt);
-    const auto& a = g.it[item];
-    const int tile = gt - g.blk_begin[item];
+    const int item = gt / g.tiles;
+    FwdArgs a = g.geo;
+    a.in = g.in[item];
+    a.anext = g.anext[item];
+    a.P = g.P[item];
+    const int tile = gt - item * g.tiles;
     const int tc = tile % a.tilesC, tr = (tile / a.tilesC) % a.tilesR, b = tile / (a.tilesC * a.tilesR);
     const int o0r = tr * FR, o0c = tc * FC;
     const int gr0 = 2 * o0r - F / 2 + 1, gc0 = 2 * o0c - F / 2 + 1;
@@ -307,22 +318,43 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
         };
         if constexpr (FT > 0) {
             constexpr int NRc = 2 * FR + FT - 2, NCc = 2 * FC + FT - 2;
-            constexpr int RW = (NRc + 3) / 4, CW = (NCc + 63) / 64; /* rows per wave, column chunks */
-            int col[CW];
+            constexpr int S0 = FWD_S0<FT>, TP = FWD_TP<FT>, W4 = TP / 4;
+            const int start = gc0 - S0; /* 16-byte aligned column of the tile's first float4 */
+            if (a.al16 && gr0 >= 0 && gr0 + NRc <= a.R && start >= 0 && start + TP <= a.C) {
+                /* interior tile: whole float4 rows [start, start + TP), every load of a thread in
+                 * flight before its first LDS write (ds_write_b128) */
+                constexpr int NE = NRc * W4, K = (NE + FB_THREADS - 1) / FB_THREADS;
+                const float* x0 = x + (int64_t)gr0 * a.C + start;
+                float4 q[K];
 #pragma unroll
-            for (int c = 0; c < CW; ++c) col[c] = colidx(min(lane + 64 * c, NCc - 1));
-            float v[RW][CW];
+                for (int k = 0; k < K; ++k) {
+                    const int e = min(k * FB_THREADS + (int)threadIdx.x, NE - 1);
+                    const int rr = e / W4, j4 = e - rr * W4;
+                    q[k] = *reinterpret_cast<const float4*>(x0 + (int64_t)rr * a.C + 4 * j4);
+                }
 #pragma unroll
-            for (int k = 0; k < RW; ++k) {
-                const float* xr = rowptr(min(wv + 4 * k, NRc - 1));
+                for (int k = 0; k < K; ++k) {
+                    const int e = k * FB_THREADS + (int)threadIdx.x;
+                    if (e < NE) reinterpret_cast<float4*>(T)[e] = q[k];
+                }
+            } else {
+                constexpr int RW = (NRc + 3) / 4, CW = (NCc + 63) / 64; /* rows per wave, column chunks */
+                int col[CW];
 #pragma unroll
-                for (int c = 0; c < CW; ++c) v[k][c] = xr[col[c]];
+                for (int c = 0; c < CW; ++c) col[c] = colidx(min(lane + 64 * c, NCc - 1));
+                float v[RW][CW];
+#pragma unroll
+                for (int k = 0; k < RW; ++k) {
+                    const float* xr = rowptr(min(wv + 4 * k, NRc - 1));
+#pragma unroll
+                    for (int c = 0; c < CW; ++c) v[k][c] = xr[col[c]];
+                }
+#pragma unroll
+                for (int k = 0; k < RW; ++k)
+#pragma unroll
+                    for (int c = 0; c < CW; ++c)
+                        if (wv + 4 * k < NRc && lane + 64 * c < NCc) T[(wv + 4 * k) * TP + S0 + lane + 64 * c] = v[k][c];
             }
-#pragma unroll
-            for (int k = 0; k < RW; ++k)
-#pragma unroll
-                for (int c = 0; c < CW; ++c)
-                    if (wv + 4 * k < NRc && lane + 64 * c < NCc) T[(wv + 4 * k) * NCc + lane + 64 * c] = v[k][c];
         } else {
             for (int rr = wv; rr < NR; rr += FB_THREADS / 64) {
                 const float* xr = rowptr(rr);
@@ -349,7 +381,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
                 const int h = it >= NCc, cc = it - h * NCc;
                 float v[NV];
 #pragma unroll
-                for (int k = 0; k < NV; ++k) v[k] = T[(2 * RH * h + k) * NCc + cc];
+                for (int k = 0; k < NV; ++k) v[k] = T[(2 * RH * h + k) * FWD_TP<FT> + FWD_S0<FT> + cc];
                 const int i0 = FT / 2 + 2 * (o0r + RH * h);
                 if (__all(i0 + 2 * (RH - 1) < a.R)) {
                     /* all RH outputs interior: tap-major, so the RH independent sums interleave */
@@ -463,20 +495,33 @@ struct InvArgs {
     int tilesC, tilesR;
 };
 
+/* the inverse's items of one geometry: per item its approximation source, packed array and output,
+ * and its threshold / zero-count words as element offsets from the geometry's thr / zc (every
+ * tensor of a call has them in one array) */
 struct InvGroup {
-    int blk_begin[FB_GROUP];
-    InvArgs it[FB_GROUP];
+    InvArgs geo;
+    int n, tiles;
+    const float* a[FB_UNI];
+    const float* P[FB_UNI];
+    float* y[FB_UNI];
+    int16_t thr_off[FB_UNI];
+    int16_t zc_off[FB_UNI];
 };
 
 template <int FT>
-__global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGroup g, Taps tp) {
+__global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGroup g, TapsT<FT> tp) {
     extern __shared__ float lds[];
     const int gt = xcd_tile(blockIdx.x, gridDim.x);
     const int F = FT ? FT : tp.F;
     const int H = F / 2;
-    const int item = find_item(g.blk_begin, gt);
-    const auto& a = g.it[item];
-    const int tile = gt - g.blk_begin[item];
+    const int item = gt / g.tiles;
+    InvArgs a = g.geo;
+    a.a = g.a[item];
+    a.P = g.P[item];
+    a.y = g.y[item];
+    a.thr = a.thr ? a.thr + g.thr_off[item] : nullptr;
+    a.zc = a.zc ? a.zc + g.zc_off[item] : nullptr;
+    const int tile = gt - item * g.tiles;
     const int tc = tile % a.tilesC, tr = (tile / a.tilesC) % a.tilesR, b = tile / (a.tilesC * a.tilesR);
     const int n0 = tr * IR, m0 = tc * IC;
     const int nl = min(n0 + IR, a.outH) - 1, ml = min(m0 + IC, a.outW) - 1;
@@ -732,7 +777,8 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
 /* dynamic LDS per workgroup; `alias`: the specialised kernels write their second-pass input
  * over their first-pass input (k_fwd_level: LH over T; k_inv_level: LoHi over Aq/Dq) */
 static size_t fwd_lds(int F, bool alias = false) {
-    const size_t t = (size_t)(2 * FR + F - 2) * (2 * FC + F - 2), lh = 2 * (size_t)FR * (2 * FC + F - 2);
+    const size_t pitch = alias ? (size_t)(3 + 2 * FC + F - 2 + 3) / 4 * 4 : (size_t)(2 * FC + F - 2); /* >= FWD_TP */
+    const size_t t = (size_t)(2 * FR + F - 2) * pitch, lh = 2 * (size_t)FR * (2 * FC + F - 2);
     return sizeof(float) * (alias ? std::max(t, lh) : t + lh);
 }
 static size_t inv_lds(int F, bool alias = false) {
@@ -741,12 +787,26 @@ static size_t inv_lds(int F, bool alias = false) {
 }
 
 template <int FT>
+static TapsT<FT> taps_of(const Taps& tp) {
+    if constexpr (FT == 0) {
+        return tp;
+    } else {
+        SmallTaps t;
+        memset(&t, 0, sizeof t);
+        t.F = tp.F;
+        for (int k = 0; k < 4; ++k)
+            for (int j = 0; j < FT; ++j) t.f[k][j] = tp.f[k][j];
+        return t;
+    }
+}
+template <int FT>
 static void fwd_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
-    hipLaunchKernelGGL(k_fwd_level<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, FT > 0), s, g, tp);
+    static_assert(FT <= SM_F_MAX, "SmallTaps holds the specialised filters");
+    hipLaunchKernelGGL(k_fwd_level<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, FT > 0), s, g, taps_of<FT>(tp));
 }
 template <int FT>
 static void inv_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
-    hipLaunchKernelGGL(k_inv_level<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F, FT > 0), s, g, tp);
+    hipLaunchKernelGGL(k_inv_level<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F, FT > 0), s, g, taps_of<FT>(tp));
 }
 
 /* The tiled path needs an even filter, the LDS budget, and images large enough that a tile
@@ -774,6 +834,7 @@ static FwdArgs fwd_args(const FwdItem& x) {
     a.last = x.last;
     a.tilesC = (a.Co + FC - 1) / FC;
     a.tilesR = (a.Ro + FR - 1) / FR;
+    a.al16 = (reinterpret_cast<uintptr_t>(x.in) % 16) == 0 && (x.C % 4) == 0;
     return a;
 }
 
@@ -800,23 +861,58 @@ static InvArgs inv_args(const InvItem& x) {
     return a;
 }
 
-/* Each launch takes up to FB_GROUP items whose tile counts sum below 2^31 (fb_tiled_ok bounds
+static_assert(sizeof(FwdGroup) + sizeof(Taps) <= 3840 && sizeof(InvGroup) + sizeof(Taps) <= 3840,
+              "filter-bank kernel arguments (plus the hidden ones) stay under 4 KB");
+
+/* Items are grouped by geometry (their order does not matter: every item is independent); each
+ * launch takes up to FB_UNI items of one geometry whose tiles sum below 2^31 (fb_tiled_ok bounds
  * every item's B * R * C below 2^31 elements, hence its tiles far below). */
+template <class Arg, class Key>
+static std::vector<std::vector<int>> uniform_groups(const std::vector<Arg>& args, const std::vector<int64_t>& tiles,
+                                                    const Key& key, int cap) {
+    std::vector<std::vector<int>> groups;
+    std::vector<int> rep; /* a representative item of each group's geometry */
+    for (int i = 0; i < (int)args.size(); ++i) {
+        int gi = -1;
+        for (int j = 0; j < (int)groups.size() && gi < 0; ++j) {
+            const int r = rep[j];
+            if ((int)groups[j].size() < cap && tiles[r] == tiles[i] && key(args[r], args[i]) &&
+                tiles[i] * (int64_t)(groups[j].size() + 1) <= INT32_MAX)
+                gi = j;
+        }
+        if (gi < 0) {
+            groups.emplace_back();
+            rep.push_back(i);
+            gi = (int)groups.size() - 1;
+        }
+        groups[gi].push_back(i);
+    }
+    return groups;
+}
+
 void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) {
-    for (int i0 = 0; i0 < n;) {
+    std::vector<FwdArgs> args(n);
+    std::vector<int64_t> tiles(n);
+    for (int i = 0; i < n; ++i) {
+        args[i] = fwd_args(it[i]);
+        tiles[i] = (int64_t)args[i].tilesC * args[i].tilesR * it[i].B;
+    }
+    auto same = [](const FwdArgs& x, const FwdArgs& y) {
+        return x.in_bs == y.in_bs && x.R == y.R && x.C == y.C && x.Ro == y.Ro && x.Co == y.Co && x.P_bs == y.P_bs &&
+               x.PC == y.PC && x.offR == y.offR && x.offC == y.offC && x.last == y.last && x.al16 == y.al16;
+    };
+    for (const auto& grp : uniform_groups(args, tiles, same, FB_UNI)) {
         FwdGroup g;
         memset(&g, 0, sizeof g);
-        int64_t blk = 0;
-        int m = 0;
-        for (; m < FB_GROUP && i0 + m < n; ++m) {
-            g.it[m] = fwd_args(it[i0 + m]);
-            const int64_t tiles = (int64_t)g.it[m].tilesC * g.it[m].tilesR * it[i0 + m].B;
-            if (m > 0 && blk + tiles > INT32_MAX) break;
-            g.blk_begin[m] = (int)blk;
-            blk += tiles;
+        g.geo = args[grp[0]];
+        g.n = (int)grp.size();
+        g.tiles = (int)tiles[grp[0]];
+        for (int m = 0; m < g.n; ++m) {
+            g.in[m] = args[grp[m]].in;
+            g.anext[m] = args[grp[m]].anext;
+            g.P[m] = args[grp[m]].P;
         }
-        for (int j = m; j < FB_GROUP; ++j) g.blk_begin[j] = INT32_MAX;
-        const int grid = (int)blk;
+        const int grid = g.n * g.tiles;
         switch (tp.F) {
         case 2: fwd_go<2>(g, grid, tp, s); break;
         case 4: fwd_go<4>(g, grid, tp, s); break;
@@ -828,25 +924,45 @@ void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) 
         case 18: fwd_go<18>(g, grid, tp, s); break;
         default: fwd_go<0>(g, grid, tp, s); break;
         }
-        i0 += m;
     }
 }
 
 void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s) {
-    for (int i0 = 0; i0 < n;) {
+    std::vector<InvArgs> args(n);
+    std::vector<int64_t> tiles(n);
+    for (int i = 0; i < n; ++i) {
+        args[i] = inv_args(it[i]);
+        tiles[i] = (int64_t)args[i].tilesC * args[i].tilesR * it[i].B;
+    }
+    /* one geometry, and the threshold / zero-count words at whole-element offsets from the
+     * group's first ones (or absent in all of them) */
+    auto off_ok = [](const void* p, const void* q, size_t elem) {
+        if ((p == nullptr) != (q == nullptr)) return false;
+        if (!p) return true;
+        const intptr_t d = reinterpret_cast<intptr_t>(q) - reinterpret_cast<intptr_t>(p);
+        return d % (intptr_t)elem == 0 && d / (intptr_t)elem >= INT16_MIN && d / (intptr_t)elem <= INT16_MAX;
+    };
+    auto same = [&](const InvArgs& x, const InvArgs& y) {
+        return x.a_bs == y.a_bs && x.lda == y.lda && x.a_from_P == y.a_from_P && x.P_bs == y.P_bs && x.PC == y.PC &&
+               x.offR == y.offR && x.offC == y.offC && x.R == y.R && x.C == y.C && x.outH == y.outH &&
+               x.outW == y.outW && off_ok(x.thr, y.thr, sizeof(float)) &&
+               off_ok(x.zc, y.zc, sizeof(unsigned long long));
+    };
+    for (const auto& grp : uniform_groups(args, tiles, same, FB_UNI)) {
         InvGroup g;
         memset(&g, 0, sizeof g);
-        int64_t blk = 0;
-        int m = 0;
-        for (; m < FB_GROUP && i0 + m < n; ++m) {
-            g.it[m] = inv_args(it[i0 + m]);
-            const int64_t tiles = (int64_t)g.it[m].tilesC * g.it[m].tilesR * it[i0 + m].B;
-            if (m > 0 && blk + tiles > INT32_MAX) break;
-            g.blk_begin[m] = (int)blk;
-            blk += tiles;
+        g.geo = args[grp[0]];
+        g.n = (int)grp.size();
+        g.tiles = (int)tiles[grp[0]];
+        for (int m = 0; m < g.n; ++m) {
+            const InvArgs& x = args[grp[m]];
+            g.a[m] = x.a;
+            g.P[m] = x.P;
+            g.y[m] = x.y;
+            g.thr_off[m] = x.thr ? (int16_t)(x.thr - g.geo.thr) : 0;
+            g.zc_off[m] = x.zc ? (int16_t)(x.zc - g.geo.zc) : 0;
         }
-        for (int j = m; j < FB_GROUP; ++j) g.blk_begin[j] = INT32_MAX;
-        const int grid = (int)blk;
+        const int grid = g.n * g.tiles;
         switch (tp.F) {
         case 2: inv_go<2>(g, grid, tp, s); break;
         case 4: inv_go<4>(g, grid, tp, s); break;
@@ -858,7 +974,6 @@ void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s) 
         case 18: inv_go<18>(g, grid, tp, s); break;
         default: inv_go<0>(g, grid, tp, s); break;
         }
-        i0 += m;
     }
 }
 

@@ -65,7 +65,6 @@ constexpr int COLLECT_IT = 16;       /* ... of 16 float4 per thread: one CHUNK  
  * launch fewer: the launch-latency regime, e.g. cfg3); larger ones launch k_window once */
 constexpr int WINDOW_INLINE_MAX_BLOCKS = 32;
 constexpr int SEG_PER_LAUNCH = 24;
-constexpr int FB_GROUP = 12;          /* images per filter-bank level launch */
 
 enum SegFlags : int32_t {
     SEG_MASK = 1,      /* level-0 / 1-D: the mask pass writes `out` from `data`   */
