@@ -2108,7 +2108,18 @@ void launch_minprune(const SegTable& t, SelHeader* head, const uint32_t* cand, w
 }
 void launch_mask_select(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
                         hipStream_t s) {
-    hipLaunchKernelGGL(k_mask_select, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, head, cand, res, thr_out);
+    bool masked = false;
+    for (int i = 0; i < t.nseg; ++i) masked = masked || (t.s[i].flags & SEG_MASK);
+    if (masked) {
+        hipLaunchKernelGGL(k_mask_select, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, head, cand, res, thr_out);
+        return;
+    }
+    /* no segment to mask (the DWT segments: the inverse thresholds on load): only the select of
+     * each segment's first block runs, so the grid is one block per segment */
+    SegTable d = t;
+    for (int i = 0; i < t.nseg; ++i) d.s[i].blk_begin = d.blk_begin[i] = i;
+    d.nblk = t.nseg;
+    hipLaunchKernelGGL(k_mask_select, dim3(d.nblk), dim3(STREAM_THREADS), 0, s, d, head, cand, res, thr_out);
 }
 void launch_mask_inplace(const SegTable& t, const wtp_result* res, const float* thr, hipStream_t s) {
     hipLaunchKernelGGL(k_mask_inplace, dim3(t.nblk), dim3(STREAM_THREADS), 0, s, t, res, thr);
