@@ -594,7 +594,8 @@ def main():
                 "bound": "hbm", "kernel": dom_kernel, "stage": dom, "launches_per_stage": dom_launches,
                 "achieved": dom_bytes / (dom_us * 1e-6) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": dom_bytes / (dom_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                "traffic": None if traffic is None else traffic * dom_launches,
+                "traffic": traffic,  # per launch, like achieved (bytes per launch / average launch)
+                "traffic_per_step": None if traffic is None else traffic * dom_launches,
                 "traffic_source": traffic_src and ("committed rocprofv3 --pmc summary %s (2 x FETCH_SIZE + "
                                                    "WRITE_SIZE per launch), not measured in this run" % traffic_src),
                 "algorithmic_bytes_per_step": dom_bytes,
@@ -604,7 +605,7 @@ def main():
                                 if dom in DWT_STAGES and work is not None else "stage inputs and outputs"),
                 "valu_frac": (work["flops_per_stage"] / (dom_us * 1e-6) / (VALU_NOFMA_TFLOPS * 1e12)
                               if dom in DWT_STAGES and work is not None else None),
-                "avg_launch_us": dom_us, "timing": timing_src,
+                "avg_launch_us": dom_us / max(dom_launches, 1), "us_per_step": dom_us, "timing": timing_src,
                 "avg_launch_us_stamps": stamps_us, "pmc_source_tag": traffic_tag},
             "stage_us": stage_us,
             "cpu_baseline": cpu,

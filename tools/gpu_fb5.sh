@@ -19,5 +19,5 @@ tail -1 "$OUT/bench_cfg5_$TAG.log" | python3 -c "
 import json,sys
 d=json.loads(sys.stdin.read()); r=d['roofline']
 print('ms/step %.3f value %.4g' % (d['ms_per_step'], d['value']), 'stages', {k: round(v,1) for k,v in d['stage_us'].items()})
-print('roofline kernel %s frac %.3f valu_frac %s achieved %.0f GB/s launches %.1f us/step %.1f traffic %s' % (r['kernel'], r['frac'], r['valu_frac'], r['achieved'], r['launches_per_stage'], r['avg_launch_us'], r['traffic']))
+print('roofline kernel %s frac %.3f valu_frac %s achieved %.0f GB/s launches %.1f us/step %.1f traffic/launch %s' % (r['kernel'], r['frac'], r['valu_frac'], r['achieved'], r['launches_per_stage'], r['us_per_step'], r['traffic']))
 print('valu_roof', d.get('valu_roof'))"

@@ -332,11 +332,12 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
                     const int rr = e / W4, j4 = e - rr * W4;
                     q[k] = *reinterpret_cast<const float4*>(x0 + (int64_t)rr * a.C + 4 * j4);
                 }
+                /* stored at the same clamped index it was loaded from (a duplicate of element
+                 * NE - 1 rewrites its own value): no predicate, so the compiler cannot sink a
+                 * load into a branch behind its own wait */
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const int e = k * FB_THREADS + (int)threadIdx.x;
-                    if (e < NE) reinterpret_cast<float4*>(T)[e] = q[k];
-                }
+                for (int k = 0; k < K; ++k)
+                    reinterpret_cast<float4*>(T)[min(k * FB_THREADS + (int)threadIdx.x, NE - 1)] = q[k];
             } else {
                 constexpr int RW = (NRc + 3) / 4, CW = (NCc + 63) / 64; /* rows per wave, column chunks */
                 int col[CW];
@@ -352,8 +353,8 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
 #pragma unroll
                 for (int k = 0; k < RW; ++k)
 #pragma unroll
-                    for (int c = 0; c < CW; ++c)
-                        if (wv + 4 * k < NRc && lane + 64 * c < NCc) T[(wv + 4 * k) * TP + S0 + lane + 64 * c] = v[k][c];
+                    for (int c = 0; c < CW; ++c) /* clamped like the loads: duplicates rewrite their own value */
+                        T[min(wv + 4 * k, NRc - 1) * TP + S0 + min(lane + 64 * c, NCc - 1)] = v[k][c];
             }
         } else {
             for (int rr = wv; rr < NR; rr += FB_THREADS / 64) {
@@ -504,8 +505,8 @@ struct InvGroup {
     const float* a[FB_UNI];
     const float* P[FB_UNI];
     float* y[FB_UNI];
-    int16_t thr_off[FB_UNI];
-    int16_t zc_off[FB_UNI];
+    int32_t thr_off[FB_UNI]; /* 32-bit: a scalar load (a 16-bit kernarg element is a vector load and a wait) */
+    int32_t zc_off[FB_UNI];
 };
 
 template <int FT>
@@ -565,11 +566,13 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
                 const int rr = e / NC_MAX, cc = e - rr * NC_MAX;
                 load4(min(rr, NRr - 1), min(cc, NCc - 1), q[k]);
             }
+            /* stored at the clamped position it was loaded from (duplicates rewrite their own
+             * value): no predicate, so no load is sunk into a branch behind its own wait */
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const int e = k * FB_THREADS + threadIdx.x;
                 const int rr = e / NC_MAX, cc = e - rr * NC_MAX;
-                if (rr < NRr && cc < NCc) store4(rr, cc, q[k]);
+                store4(min(rr, NRr - 1), min(cc, NCc - 1), q[k]);
             }
         } else {
             for (int e = threadIdx.x; e < NRr * NCc; e += FB_THREADS) {
@@ -959,8 +962,8 @@ void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s) 
             g.a[m] = x.a;
             g.P[m] = x.P;
             g.y[m] = x.y;
-            g.thr_off[m] = x.thr ? (int16_t)(x.thr - g.geo.thr) : 0;
-            g.zc_off[m] = x.zc ? (int16_t)(x.zc - g.geo.zc) : 0;
+            g.thr_off[m] = x.thr ? (int32_t)(x.thr - g.geo.thr) : 0;
+            g.zc_off[m] = x.zc ? (int32_t)(x.zc - g.geo.zc) : 0;
         }
         const int grid = g.n * g.tiles;
         switch (tp.F) {
