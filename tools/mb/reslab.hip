@@ -111,7 +111,7 @@ int main(int argc, char** argv) {
     printf("k_resident cfg2: median %.2f us (min %.2f) per call, %.1f GB/s algorithmic\n", tms[tms.size() / 2], tms[0],
            8.0 * nw / (tms[tms.size() / 2] * 1e-6) / 1e9);
     const char* names[18] = {"start", "window", "counted", "hist-pub", "B1-arrive", "B1-pass", "selected", "stored",
-                             "sampled", "spec-stored", "issued", "loaded", "w:cleared", "w:histo", "w:scanned",
+                             "sampled", "sorted", "issued", "published", "w:cleared", "w:histo", "w:scanned",
                              "w:found", "sc:placed", "sc:issued"};
     for (int p = 0; p < 18; ++p) {
         std::vector<double> med, mx;
@@ -119,7 +119,7 @@ int main(int argc, char** argv) {
         std::sort(med.begin(), med.end()); std::sort(mx.begin(), mx.end());
         printf("  %-10s median WG %7.2f us   slowest WG %7.2f us\n", names[p], med[med.size() / 2], mx[mx.size() / 2]);
     }
-    const char* snames[15] = {"-", "counters", "buckets", "B2-arrive", "B2-pass", "staged", "ranks", "-", "-", "-", "-", "-", "-", "-", "-"};
+    const char* snames[15] = {"-", "counters", "buckets", "B2-wait", "B2-pass", "staged", "ranks", "-", "-", "-", "-", "-", "-", "-", "-"};
     for (int p = 0; p < 15; ++p) {
         if (p == 0 || p >= 7) continue;
         std::sort(sel[p].begin(), sel[p].end());

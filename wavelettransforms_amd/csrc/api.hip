@@ -214,7 +214,7 @@ Layout make_layout(std::vector<TPlan>& ps) {
     L.cand = off;
     size_t ce = 0;
     for (auto& p : ps) { p.cand_off = ce; ce += (size_t)p.cap; }
-    /* a resident launch (k_resident) keeps one run of RES_WG_WORDS per workgroup there instead */
+    /* a resident launch (k_resident) keeps one published region of RES_WG_WORDS per workgroup there instead */
     int64_t rwg = 0;
     for (auto& p : ps)
         if (!p.dwt) rwg += (p.pop + RES_CHUNK - 1) / RES_CHUNK;

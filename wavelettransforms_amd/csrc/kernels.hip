@@ -47,6 +47,21 @@ template <class T>
 __device__ __forceinline__ void stc(T* p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+/* a 16-byte write-through (sc1) vector store: MI355X_MICROARCH.md's hand-off form for tens of KB
+ * per workgroup (drained by the storer's vmcnt(0) before its arrival, read with sc1 loads).  A
+ * buffer store through the builtin (cache policy 16 = sc1), not inline asm: the compiler then
+ * knows the store reads its data VGPRs late and keeps the wait state before they are rewritten
+ * (an inline-asm dwordx4 store had its data registers overwritten by the next VALU op). */
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t region_rsrc(const uint32_t* p, int words) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, words * 4, 0x00020000);
+}
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, int word, uint4 v) {
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    const u4v x = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, 4 * word, 0, 16);
+}
 
 __device__ __forceinline__ int find_seg(const SegTable& t, int b) {
     int s = 0; /* blk_begin[0] == 0; entries past nseg hold INT32_MAX */
@@ -1231,7 +1246,10 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     WTP_RPROBE(0);
     __shared__ uint32_t s_win[3];
     __shared__ uint32_t s_sync; /* the sampling waves' LDS meeting counter */
+    __shared__ uint32_t s_pubn; /* the storing waves drained (publication) */
+    __shared__ uint32_t s_arr;  /* wave 7's first-level parity arrival */
     float4 v[IT];
+    uint32_t arr1 = 0; /* wave 7 lane 0: the first-level parity arrival's result */
     /* ---- P0: the sample waves' loads go out before any chunk load of the workgroup (the barrier
      * below orders them), then every wave issues its chunk; the sample arrives first (a wave's
      * loads return in order) and is histogrammed while the chunk streams in; wave 0 searches the
@@ -1253,7 +1271,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         }
         for (int j = tid; j < RES_HBINS; j += CT) raw[j] = 0u;
         for (int j = tid; j < RES_NSUB; j += CT) lsub[j] = 0u;
-        if (tid == 0) s_sync = 0u;
+        if (tid == 0) { s_sync = 0u; s_pubn = 0u; }
         if (first && tid == 0) { /* memory-side words: later adds come from other workgroups */
             stc(reinterpret_cast<unsigned long long*>(&res[sd.res].zero_count), 0ull);
             stc(&res[sd.res].path, 0);
@@ -1291,6 +1309,10 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         }
         if (FULL) load_chunk<IT, CT>(sd.data + base, v);
         else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
+        /* the parity flip's first-level arrival (the last reader of the parity in the grid flips
+         * it): a returning add issued behind wave 7's chunk loads, its result used only at the
+         * publication, so its queueing on the shard's counter costs no wave a wait */
+        if (wv == NW - 1 && lane == 0) arr1 = atomicAdd(&bar_region(head, q)->arrive[blockIdx.x & (NSHARD - 1)][0], 1u);
         WTP_RPROBE(10);
     }
     __syncthreads();
@@ -1332,6 +1354,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     }
     __syncthreads();
     WTP_RPROBE(2);
+    if (wv == NW - 1 && lane == 0) s_arr = arr1;
     uint32_t wmax = 0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) wmax = max(wmax, wred[w][5]);
@@ -1375,21 +1398,110 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     uint32_t* b1 = reinterpret_cast<uint32_t*>(&st->seg_bar[1]);
     uint32_t* b2 = reinterpret_cast<uint32_t*>(&st->seg_bar[2]);
     res_arrive(b1);
-    /* the grid's last arrival flips the region parity (every workgroup has read it by then):
-     * lane 0 of wave 1, off the polling lane's path, through per-shard counters (blockIdx % 8;
-     * the last arriver of a shard adds to the top counter) so no address queues more than
-     * ~gridDim / 8 returning adds */
-    if (tid == 64) {
-        const uint32_t sh8 = blockIdx.x & (NSHARD - 1);
-        const uint32_t nsh = (gridDim.x - sh8 + NSHARD - 1) / NSHARD;
-        const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);
-        if (atomicAdd(&bar->arrive[sh8][0], 1u) == nsh - 1u && atomicAdd(&bar->arrive[0][16], 1u) == nact - 1u)
-            stc(&head->parity, q ^ 1u);
-    }
     WTP_RPROBE(4);
-    if (!res_wait(b1, nwg, tmo)) {
+    /* ---- publication, while the segment gathers at barrier 1: this workgroup's inside keys,
+     * bucket-sorted in LDS, and the bucket offsets (exclusive prefix of its bucket histogram),
+     * write-through (16-byte sc1 stores) to its region of the candidate area, then barrier 2's
+     * arrival.  It depends on nothing global: waves 0-6 store and drain it while wave 7 polls
+     * barrier 1, and after barrier 1 the select reads only the keys of the ranks' buckets from
+     * the regions (offsets, then keys: two round trips) -- no slot round after the locate. */
+    uint32_t* pub = cand + (int64_t)blockIdx.x * RES_PUB_WORDS;
+    uint32_t* pos = raw;     /* bucket offsets (the window histogram is done with) */
+    uint32_t* srt = wstage;  /* the sorted keys, over the columns */
+    __shared__ uint32_t s_ok1;
+    if (!ovf) { /* block-uniform */
+        uint32_t kk[RES_STG];
+#pragma unroll
+        for (int j = 0; j < RES_STG; ++j) kk[j] = col[j * CT]; /* entries past cnt are not used */
+        /* exclusive scan of the bucket counts, BPT buckets per thread */
+        __shared__ uint32_t s_pw[NW];
+        uint32_t c[BPT], cs = 0;
+#pragma unroll
+        for (int j = 0; j < BPT; ++j) { c[j] = lsub[BPT * tid + j]; cs += c[j]; }
+        const uint32_t inc = wave_scan_u32(cs);
+        if (lane == 63) s_pw[wv] = inc;
+        __syncthreads(); /* also: every column is read into kk */
+        uint32_t ex = inc - cs;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) ex += w < wv ? s_pw[w] : 0u;
+#pragma unroll
+        for (int j = 0; j < BPT; ++j) { pos[BPT * tid + j] = ex; ex += c[j]; }
+        __syncthreads();
+        /* scatter, four keys at a time with no branch (a key past cnt counts into its lane's
+         * spare counter pos[RES_NSUB + lane] -- one per lane: a shared one serialised every
+         * atomic 64 ways -- and lands in the spare words past the sorted array): the four
+         * returning atomics issue back to back; the trip count is the wave's largest cnt */
+        const uint32_t wc = wred[wv][5];
+#pragma unroll
+        for (int j0 = 0; j0 < RES_STG; j0 += 4) {
+            if ((uint32_t)j0 < wc) {
+                uint32_t pp[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const bool ok = (uint32_t)(j0 + u) < cnt;
+                    pp[u] = atomicAdd(&pos[ok ? (kk[j0 + u] - kl) >> sh : (uint32_t)(RES_NSUB + lane)], 1u);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const bool ok = (uint32_t)(j0 + u) < cnt;
+                    srt[ok ? pp[u] : (uint32_t)(RES_STG * CT + lane)] = kk[j0 + u];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    WTP_RPROBE(9);
+    if (wv == NW - 1) {
+        /* ---- barrier 1, polled by wave 7 while the others store */
+        if (lane == 0) {
+            const uint64_t t0 = wall_ticks();
+            uint32_t ok = 0;
+            while (true) {
+                const uint32_t x = ldc<true>(b1);
+                if (x & RES_POISON) break;
+                if (x >= nwg) { ok = 1; break; }
+                if (wall_ticks() - t0 > tmo) {
+                    if (atomicCAS(b1, x, x | RES_POISON) == x) break;
+                    continue; /* it moved: look again */
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_ok1 = ok;
+        }
+    } else {
+        constexpr int ST = CT - 64; /* the storing threads */
+        if (!ovf) {
+            /* offsets: pub[b] = start of bucket b (pos[b - 1] now), pub[RES_NSUB] = the total */
+            const __amdgpu_buffer_rsrc_t prs = region_rsrc(pub, RES_PUB_WORDS);
+            if (tid < RES_NSUB / 4) {
+                const int b = 4 * tid;
+                st16_sc1(prs, b, make_uint4(b ? pos[b - 1] : 0u, pos[b], pos[b + 1], pos[b + 2]));
+            } else if (tid == RES_NSUB / 4) {
+                stc(pub + RES_NSUB, pos[RES_NSUB - 1]);
+            }
+            const uint32_t nin = pos[RES_NSUB - 1];
+            for (uint32_t i4 = tid; 4 * i4 < nin; i4 += ST)
+                st16_sc1(prs, RES_PUB_KEYS + 4 * i4, *reinterpret_cast<const uint4*>(srt + 4 * i4));
+        }
+        /* every storing wave drains; the last one to do so arrives at barrier 2 for the
+         * workgroup (its LDS add follows every other storing wave's drain) */
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0 && atomicAdd(&s_pubn, 1u) == (uint32_t)(NW - 2)) atomicAdd(b2, 1u);
+        /* the parity flip's second level: the last reader of a shard (blockIdx % 8) adds to the
+         * top counter, whose last arrival flips the parity (every workgroup of the grid has read
+         * it) -- wave 6, after its drain, off the barrier-1 poll */
+        if (wv == NW - 2 && lane == 0) {
+            const uint32_t sh8 = blockIdx.x & (NSHARD - 1);
+            const uint32_t nsh = (gridDim.x - sh8 + NSHARD - 1) / NSHARD;
+            const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);
+            if (s_arr == nsh - 1u && atomicAdd(&bar->arrive[0][16], 1u) == nact - 1u) stc(&head->parity, q ^ 1u);
+        }
+    }
+    __syncthreads();
+    WTP_RPROBE(11);
+    if (!s_ok1) {
         if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
-        return; /* nothing stored: the caller's input and output are untouched */
+        return; /* nothing stored to the output: the caller's input and output are untouched */
     }
     WTP_RPROBE(5);
     /* ---- P2: the segment's counters and bucket totals in one round trip (every load in
@@ -1478,80 +1590,61 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         if (m > RES_SEL_MAX) {
             full = true; /* uniform over the segment: the same totals everywhere */
         } else {
-            /* ---- this workgroup's keys of buckets ba / bb into its slot (sc1 stores) */
-            __shared__ uint32_t s_fill;
-            if (tid == 0) s_fill = 0;
-            __syncthreads();
-            uint32_t* slot = cand + (int64_t)blockIdx.x * RES_SLOT_WORDS;
-            for (uint32_t j0 = 0; j0 < cnt; j0 += 8) {
-                uint32_t kk[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) kk[u] = col[min(j0 + u, (uint32_t)RES_STG) * CT];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int bk = (int)((kk[u] - kl) >> sh);
-                    if (j0 + u < cnt && (bk == ba || bk == bb)) {
-                        const uint32_t p = atomicAdd(&s_fill, 1u);
-                        if (p < (uint32_t)RES_SLOT_CAP) stc(slot + 1 + p, kk[u]);
-                    }
-                }
-            }
-            __syncthreads();
-            if (tid == 0) stc(slot, s_fill);
-            /* ---- segment barrier 2: every slot of the segment is written */
-            res_arrive(b2);
+            /* ---- barrier 2: every region of the segment is published (its arrivals were made
+             * before barrier 1's wait, so this wait is short) */
             WTP_PROBE(3);
             if (!res_wait(b2, nwg, tmo)) {
                 if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
                 return;
             }
             WTP_PROBE(4);
-            /* ---- the segment's slots (consecutive in the candidate region) in one round trip
-             * per four words a thread, copied raw into LDS (the columns are done with) */
+            /* ---- the segment's workgroups' offsets of buckets ba and bb + 1 (wave 0, every load
+             * in flight at once), their key counts scanned; then the keys themselves, at most two
+             * a thread (m <= RES_SEL_MAX), staged in LDS.  The buckets between ba and bb are
+             * empty, so a workgroup's keys of ba..bb are one run of its sorted array. */
             const int wb = sd.blk_begin;
-            const int nwords = (int)nwg * RES_SLOT_WORDS;
-            const uint32_t* sl = cand + (int64_t)wb * RES_SLOT_WORDS;
-            uint32_t* rawsl = wstage;
-            for (int i0 = tid; i0 < nwords; i0 += 4 * CT) {
-                uint32_t kv[4];
+            __shared__ uint32_t s_so[RES_MAX_WG], s_ob[RES_MAX_WG];
+            __shared__ uint32_t s_tot;
+            if (wv == 0) {
+                constexpr int WPL = RES_MAX_WG / 64;
+                uint32_t ob[WPL], oe[WPL];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) kv[u] = i0 + u * CT < nwords ? ldc<true>(sl + i0 + u * CT) : 0u;
+                for (int u = 0; u < WPL; ++u) {
+                    const int w = lane + 64 * u;
+                    const uint32_t* pw = cand + (int64_t)(wb + min(w, (int)nwg - 1)) * RES_PUB_WORDS;
+                    ob[u] = ldc<true>(pw + ba);
+                    oe[u] = ldc<true>(pw + bb + 1);
+                }
+                uint32_t base = 0;
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (i0 + u * CT < nwords) rawsl[i0 + u * CT] = kv[u];
+                for (int u = 0; u < WPL; ++u) {
+                    const int w = lane + 64 * u;
+                    const uint32_t cw = w < (int)nwg ? oe[u] - ob[u] : 0u;
+                    const uint32_t inc = wave_scan_u32(cw);
+                    if (w < (int)nwg) { s_so[w] = base + inc - cw; s_ob[w] = ob[u]; }
+                    base += __builtin_amdgcn_readlane(inc, 63);
+                }
+                if (lane == 0) s_tot = base;
             }
             __syncthreads();
-            __shared__ uint32_t s_so[RES_MAX_WG];
-            __shared__ uint32_t s_tot, s_sovf;
-            if (wv == 0) { /* exclusive scan of the slot counts, four slots per lane */
-                uint32_t c4[RES_MAX_WG / 64], s4 = 0, o4 = 0;
-#pragma unroll
-                for (int u = 0; u < RES_MAX_WG / 64; ++u) {
-                    const int w = 4 * lane + u;
-                    c4[u] = w < (int)nwg ? rawsl[w * RES_SLOT_WORDS] : 0u;
-                    o4 |= c4[u] > (uint32_t)RES_SLOT_CAP ? 1u : 0u;
-                    s4 += c4[u];
-                }
-                const uint32_t inc4 = wave_scan_u32(s4);
-                uint32_t o = inc4 - s4;
-#pragma unroll
-                for (int u = 0; u < RES_MAX_WG / 64; ++u) {
-                    const int w = 4 * lane + u;
-                    if (w < (int)nwg) s_so[w] = o;
-                    o += c4[u];
-                }
-                const uint64_t ob = __ballot(o4 != 0);
-                if (lane == 63) s_tot = inc4;
-                if (lane == 0) s_sovf = ob != 0;
-            }
-            __syncthreads();
-            if (s_sovf || (int)s_tot != m) {
-                full = true; /* a slot overflowed: uniform over the segment (same slots everywhere) */
+            if ((int)s_tot != m) {
+                full = true; /* uniform over the segment (the same regions everywhere) */
             } else {
-                for (int i = tid; i < nwords; i += CT) {
-                    const int w = i / RES_SLOT_WORDS, j = i % RES_SLOT_WORDS;
-                    if (j >= 1 && (uint32_t)j <= rawsl[w * RES_SLOT_WORDS]) stage[s_so[w] + j - 1] = rawsl[i];
+                uint32_t kv[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int i = min(tid + u * CT, m - 1);
+                    int lo_w = 0, hi_w = (int)nwg - 1; /* the last workgroup whose run starts <= i */
+                    while (lo_w < hi_w) {
+                        const int mid = (lo_w + hi_w + 1) >> 1;
+                        if (s_so[mid] <= (uint32_t)i) lo_w = mid; else hi_w = mid - 1;
+                    }
+                    kv[u] = ldc<true>(cand + (int64_t)(wb + lo_w) * RES_PUB_WORDS + RES_PUB_KEYS + s_ob[lo_w] +
+                                      ((uint32_t)i - s_so[lo_w]));
                 }
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    if (tid + u * CT < m) stage[tid + u * CT] = kv[u];
                 __syncthreads();
                 WTP_PROBE(5);
                 /* ---- the ranks among the staged keys (buckets ba..bb; buckets between are empty:
@@ -1665,7 +1758,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader*
     __shared__ __attribute__((aligned(16))) uint32_t raw[RES_HBINS > RES_SEL_MAX ? RES_HBINS : RES_SEL_MAX];
     __shared__ uint32_t lsub[RES_NSUB];
     __shared__ uint32_t wred[RES_THREADS / 64][8];
-    __shared__ uint32_t wstage[(RES_STG + 1) * RES_THREADS]; /* 66 KB: RES_STG slots + the discard slot per thread */
+    __shared__ __attribute__((aligned(16))) uint32_t wstage[(RES_STG + 1) * RES_THREADS]; /* 66 KB: RES_STG slots + the discard slot per thread */
     const uint32_t q = head->parity;
     if (t.stamps && threadIdx.x == 0) atomicMin(t.stamps, wall_ticks()); /* measurement only */
     {   /* clear this workgroup's slice of the idle region (the previous launch's) */

@@ -188,9 +188,11 @@ constexpr int RES_MAX_WG = 256;                     /* workgroups a resident lau
 constexpr int RES_STG = 32;                         /* inside keys a thread may stage (of its 96; ~11 expected) */
 /* After the first segment barrier every workgroup publishes the keys of the (one or two)
  * buckets holding the segment's ranks in a slot of its own: word 0 the count, then the keys */
-constexpr int RES_SLOT_WORDS = 32;
-constexpr int RES_SLOT_CAP = RES_SLOT_WORDS - 1;
-constexpr int RES_WG_WORDS = RES_SLOT_WORDS;        /* one workgroup's slot in the candidate region */
+/* one workgroup's published region in the candidate area: its bucket offsets (RES_NSUB + 1 words,
+ * padded to 16 bytes), then its inside keys bucket-sorted (at most RES_STG per thread) */
+constexpr int RES_PUB_KEYS = (RES_NSUB + 1 + 3) / 4 * 4;
+constexpr int RES_PUB_WORDS = RES_PUB_KEYS + RES_STG * RES_THREADS;
+constexpr int RES_WG_WORDS = RES_PUB_WORDS;
 constexpr int RES_SEL_MAX = 1024;                   /* keys the one-wave select takes (more: full scan) */
 constexpr uint32_t RES_TIMEOUT_DEFAULT_US = 200000; /* a wait this long means the grid is not co-resident */
 int resident_capacity();
