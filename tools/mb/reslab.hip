@@ -3,9 +3,10 @@
 // of k_resident (WTP_RPROBE).  Not part of the product.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off reslab.hip -o reslab
 #include <hip/hip_runtime.h>
-__device__ unsigned long long g_rprobe[256][20];
-__device__ unsigned long long g_cyc[256][2];
-__device__ unsigned long long g_sprobe[256][16];
+#define NWG 256
+__device__ unsigned long long g_rprobe[NWG][20];
+__device__ unsigned long long g_cyc[NWG][2];
+__device__ unsigned long long g_sprobe[NWG][16];
 #ifndef RESLAB_NOPROBE
 #define WTP_RPROBE(i) do { if (threadIdx.x == 0) { g_rprobe[blockIdx.x][i] = wall_clock64(); \
     if ((i) == 0) g_cyc[blockIdx.x][0] = __builtin_amdgcn_s_memtime(); \
@@ -13,6 +14,7 @@ __device__ unsigned long long g_sprobe[256][16];
 #define WTP_PROBE(i) do { if (threadIdx.x == 0) g_sprobe[blockIdx.x][i] = wall_clock64(); } while (0)
 #define WTP_PROBE_T(i, t) do { if (threadIdx.x == (t)) g_sprobe[blockIdx.x][i] = wall_clock64(); } while (0)
 #define WTP_WPROBE(i) WTP_RPROBE(12 + (i))
+#define WTP_RTAG(tagv) do { if (threadIdx.x == 0) g_rprobe[blockIdx.x][19] = (unsigned long long)(tagv); } while (0)
 #endif
 #include "../../wavelettransforms_amd/csrc/kernels.hip"
 #include "../../wavelettransforms_amd/csrc/filterbank.hip"
@@ -51,8 +53,9 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 5; ++i) if (wtp_prune_layers_f32(ts.data(), 20, wid, 5, 50.0, ws, wsb, res, 0)) { printf("err %s\n", wtp_last_error()); return 1; }
     CK(hipDeviceSynchronize());
     std::vector<float> tms;
-    unsigned long long pr[256][20];
-    std::vector<std::vector<double>> ph(18), sel(15);
+    static unsigned long long pr[NWG][20];
+    std::vector<std::vector<double>> ph(18), sel(15), phg[2];
+    phg[0].resize(18); phg[1].resize(18);
     for (int r = 0; r < reps; ++r) {
         CK(hipEventRecord(a, 0));
         wtp_prune_layers_f32(ts.data(), 20, wid, 5, 50.0, ws, wsb, res, 0);
@@ -60,7 +63,7 @@ int main(int argc, char** argv) {
         CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b)); tms.push_back(ms * 1000);
         CK(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_rprobe), sizeof pr));
-        unsigned long long sp[256][16];
+        static unsigned long long sp[NWG][16];
         CK(hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_sprobe), sizeof sp));
         int nb = 0; for (int t = 0; t < 20; ++t) { int64_t n = 1; for (int d = 0; d < 4; ++d) n *= shapes[t][d]; nb += (int)((n + RES_CHUNK - 1) / RES_CHUNK); }
         unsigned long long t0 = ~0ull;
@@ -73,11 +76,20 @@ int main(int argc, char** argv) {
             sel[p].push_back(v.empty() ? -1 : v[v.size() / 2]);
         }
         for (int p = 0; p < 18; ++p) {
-            std::vector<double> v;
-            for (int i = 0; i < nb; ++i) v.push_back((double)(pr[i][p] - t0) / 100.0);
+            std::vector<double> v, vg[2];
+            for (int i = 0; i < nb; ++i) {
+                const double x = (double)(pr[i][p] - t0) / 100.0;
+                v.push_back(x);
+                vg[(pr[i][19] & 16) ? 1 : 0].push_back(x);
+            }
             std::sort(v.begin(), v.end());
             ph[p].push_back(v[v.size() / 2]);
             ph[p].push_back(v.back());
+            for (int g = 0; g < 2; ++g) {
+                std::sort(vg[g].begin(), vg[g].end());
+                phg[g][p].push_back(vg[g].empty() ? -1 : vg[g][vg[g].size() / 2]);
+                phg[g][p].push_back(vg[g].empty() ? -1 : vg[g].back());
+            }
         }
     }
     {   /* the last rep's probes of every workgroup, for offline analysis */
@@ -86,17 +98,17 @@ int main(int argc, char** argv) {
             int nb = 0; for (int t = 0; t < 20; ++t) { int64_t n = 1; for (int d = 0; d < 4; ++d) n *= shapes[t][d]; nb += (int)((n + RES_CHUNK - 1) / RES_CHUNK); }
             unsigned long long t0 = ~0ull;
             for (int i = 0; i < nb; ++i) t0 = std::min(t0, pr[i][0]);
-            fprintf(f, "wg,start,window,counted,reserved,scattered,barrier,selected,stored,sampled,specstored\n");
+            fprintf(f, "wg,late,start,window,counted,hist-pub,B1-arrive,B1-pass,selected,stored,sampled,sorted,issued,published\n");
             for (int i = 0; i < nb; ++i) {
-                fprintf(f, "%d", i);
-                for (int p = 0; p < 10; ++p) fprintf(f, ",%.2f", (double)(pr[i][p] - t0) / 100.0);
+                fprintf(f, "%d,%d", i, (int)((pr[i][19] >> 4) & 1));
+                for (int p = 0; p < 12; ++p) fprintf(f, ",%.2f", (double)(pr[i][p] - t0) / 100.0);
                 fprintf(f, "\n");
             }
             fclose(f);
         }
     }
     {
-        unsigned long long cy[256][2];
+        static unsigned long long cy[NWG][2];
         CK(hipMemcpyFromSymbol(cy, HIP_SYMBOL(g_cyc), sizeof cy));
         int nb = 0; for (int t = 0; t < 20; ++t) { int64_t n = 1; for (int d = 0; d < 4; ++d) n *= shapes[t][d]; nb += (int)((n + RES_CHUNK - 1) / RES_CHUNK); }
         std::vector<double> f;
@@ -117,7 +129,14 @@ int main(int argc, char** argv) {
         std::vector<double> med, mx;
         for (size_t i = 0; i < ph[p].size(); i += 2) { med.push_back(ph[p][i]); mx.push_back(ph[p][i + 1]); }
         std::sort(med.begin(), med.end()); std::sort(mx.begin(), mx.end());
-        printf("  %-10s median WG %7.2f us   slowest WG %7.2f us\n", names[p], med[med.size() / 2], mx[mx.size() / 2]);
+        printf("  %-10s median WG %7.2f us   slowest WG %7.2f us", names[p], med[med.size() / 2], mx[mx.size() / 2]);
+        for (int g = 0; g < 2; ++g) {
+            std::vector<double> gm, gx;
+            for (size_t i = 0; i < phg[g][p].size(); i += 2) { gm.push_back(phg[g][p][i]); gx.push_back(phg[g][p][i + 1]); }
+            std::sort(gm.begin(), gm.end()); std::sort(gx.begin(), gx.end());
+            printf("   | %s median %6.2f slowest %6.2f", g ? "late" : "early", gm[gm.size() / 2], gx[gx.size() / 2]);
+        }
+        printf("\n");
     }
     const char* snames[15] = {"-", "counters", "buckets", "B2-wait", "B2-pass", "staged", "ranks", "-", "-", "-", "-", "-", "-", "-", "-"};
     for (int p = 0; p < 15; ++p) {

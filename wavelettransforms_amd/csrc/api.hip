@@ -650,6 +650,21 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         const int64_t chunk = resident ? RES_CHUNK : CHUNK;
         SegTable tab;
         memset(&tab, 0, sizeof tab);
+        /* the resident launch's late group: the smallest segments, together at most RES_LATE_PCT %
+         * of the workgroups (at least one segment stays early) */
+        bool late[SEG_PER_LAUNCH] = {};
+        if (resident) {
+            int by[SEG_PER_LAUNCH];
+            for (int i = 0; i < g1 - g0; ++i) by[i] = g0 + i;
+            std::stable_sort(by, by + (g1 - g0), [&](int a, int b) { return ps[a].pop < ps[b].pop; });
+            int64_t lb = 0;
+            for (int i = 0; i + 1 < g1 - g0; ++i) {
+                const int64_t w = (ps[by[i]].pop + RES_CHUNK - 1) / RES_CHUNK;
+                if (100 * (lb + w) > (int64_t)RES_LATE_PCT * rblk) break;
+                lb += w;
+                late[by[i] - g0] = true;
+            }
+        }
         int blk = 0;
         for (int t = g0; t < g1; ++t) {
             const TPlan& p = ps[t];
@@ -671,6 +686,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             sd.cap = p.cap;
             bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap, p.dwt);
             if (resident) sd.nsub_log2 = RES_NSUB_LOG2;
+            if (late[t - g0]) sd.flags |= SEG_LATE;
             blk += (int)((p.pop + chunk - 1) / chunk);
         }
         tab.nblk = blk;

@@ -220,6 +220,9 @@ __device__ __forceinline__ void wave_pick_digit(const uint32_t* hb, int64_t r, i
 #ifndef WTP_WPROBE
 #define WTP_WPROBE(i)
 #endif
+#ifndef WTP_RTAG /* k_resident: the workgroup's segment flags, for the phase lab */
+#define WTP_RTAG(tagv)
+#endif
 #ifndef WTP_GPROBE /* a probe taken by lane 0 of the executing wave */
 #define WTP_GPROBE(i)
 #endif
@@ -1244,6 +1247,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const uint64_t tmo = t.res_timeout;
     WTP_RPROBE(0);
+    WTP_RTAG(sd.flags);
     __shared__ uint32_t s_win[3];
     __shared__ uint32_t s_sync; /* the sampling waves' LDS meeting counter */
     __shared__ uint32_t s_pubn; /* the storing waves drained (publication) */
@@ -1307,6 +1311,10 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 WTP_RPROBE(1);
             }
         }
+        /* a late workgroup (SEG_LATE: the group's small segments) issues its chunk only once
+         * the window is known: the early group's chunks come off HBM first, and their counts,
+         * barriers and selects run while the late group's chunks stream */
+        if (sd.flags & SEG_LATE) __syncthreads(); /* block-uniform */
         if (FULL) load_chunk<IT, CT>(sd.data + base, v);
         else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
         /* the parity flip's first-level arrival (the last reader of the parity in the grid flips
@@ -1360,15 +1368,28 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     for (int w = 0; w < NW; ++w) wmax = max(wmax, wred[w][5]);
     /* block-uniform: a thread's column overflowed -> the segment takes the full scan */
     const bool ovf = wmax > (uint32_t)RES_STG;
+    /* a segment of ONE workgroup (solo) selects from its own LDS: no counter, bucket total,
+     * publication or barrier touches memory -- under the launch's traffic every round trip costs
+     * 1-3 us, and the solo segments were the launch's tail */
+    const uint32_t nwg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
+    const bool solo = nwg == 1u; /* block-uniform */
+    __shared__ unsigned long long s_cnt[1];
+    __shared__ uint32_t s_mk, s_ovf;
     if (tid == 0) {
         unsigned long long a0 = 0;
         uint32_t m2 = 0;
         for (int w = 0; w < NW; ++w) { a0 += wred[w][0]; m2 = max(m2, wred[w][2]); }
         if (kl > 0) a0 -= (unsigned long long)(RES_CHUNK - len);
-        const int sh8 = blockIdx.x & (NSHARD - 1);
-        if (a0) atomicAdd(&st->below[sh8], a0);
-        atomicMax(&st->maxkey[sh8], m2);
-        if (ovf) atomicOr(&st->overflow, 1u);
+        if (solo) {
+            s_cnt[0] = a0;
+            s_mk = m2;
+            s_ovf = ovf;
+        } else {
+            const int sh8 = blockIdx.x & (NSHARD - 1);
+            if (a0) atomicAdd(&st->below[sh8], a0);
+            atomicMax(&st->maxkey[sh8], m2);
+            if (ovf) atomicOr(&st->overflow, 1u);
+        }
     }
     /* the inside keys' bucket histogram in LDS (eight column reads in flight per step), then the
      * segment's bucket totals as no-return atomic adds */
@@ -1384,20 +1405,21 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 if (j0 + u < cnt) atomicAdd(&lsub[(kk[u] - kl) >> sh], 1u);
         }
         __syncthreads();
+        if (!solo) {
 #pragma unroll
-        for (int j = 0; j < BPT; ++j) { /* bucket j * CT + tid: 256 contiguous bytes per wave instruction */
-            const uint32_t c = lsub[j * CT + tid];
-            if (c) atomicAdd(&st->sub[j * CT + tid], c);
+            for (int j = 0; j < BPT; ++j) { /* bucket j * CT + tid: 256 contiguous bytes per wave instruction */
+                const uint32_t c = lsub[j * CT + tid];
+                if (c) atomicAdd(&st->sub[j * CT + tid], c);
+            }
         }
     }
     WTP_RPROBE(3);
     /* ---- segment barrier 1: every workgroup's counters and bucket totals are in */
     BarState* bar = bar_region(head, q);
-    const uint32_t nwg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
     uint32_t* b0 = reinterpret_cast<uint32_t*>(&st->seg_bar[0]);
     uint32_t* b1 = reinterpret_cast<uint32_t*>(&st->seg_bar[1]);
     uint32_t* b2 = reinterpret_cast<uint32_t*>(&st->seg_bar[2]);
-    res_arrive(b1);
+    if (!solo) res_arrive(b1);
     WTP_RPROBE(4);
     /* ---- publication, while the segment gathers at barrier 1: this workgroup's inside keys,
      * bucket-sorted in LDS, and the bucket offsets (exclusive prefix of its bucket histogram),
@@ -1451,7 +1473,16 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         __syncthreads();
     }
     WTP_RPROBE(9);
-    if (wv == NW - 1) {
+    if (solo) {
+        /* the parity flip's second level (as the storing waves do it below) */
+        if (tid == 64 * (NW - 2)) {
+            const uint32_t sh8 = blockIdx.x & (NSHARD - 1);
+            const uint32_t nsh = (gridDim.x - sh8 + NSHARD - 1) / NSHARD;
+            const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);
+            if (s_arr == nsh - 1u && atomicAdd(&bar->arrive[0][16], 1u) == nact - 1u) stc(&head->parity, q ^ 1u);
+        }
+        if (tid == 0) s_ok1 = 1;
+    } else if (wv == NW - 1) {
         /* ---- barrier 1, polled by wave 7 while the others store */
         if (lane == 0) {
             const uint64_t t0 = wall_ticks();
@@ -1506,11 +1537,10 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     WTP_RPROBE(5);
     /* ---- P2: the segment's counters and bucket totals in one round trip (every load in
      * flight before any is used); a block scan of the totals names the bucket of each rank */
-    __shared__ unsigned long long s_cnt[1];
-    __shared__ uint32_t s_mk, s_ovf, s_wtot[NW];
+    __shared__ uint32_t s_wtot[NW], s_b2;
     __shared__ int s_bk[2];
     __shared__ uint32_t s_bef[2], s_bn[2];
-    {
+    if (!solo) {
         if (tid == 0) {
             unsigned long long x[NSHARD];
 #pragma unroll
@@ -1529,12 +1559,16 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             s_mk = mm;
         } else if (tid == 3) {
             s_ovf = ldc<true>(&st->overflow);
+        } else if (tid == 4) {
+            /* barrier 2's counter in the same round trip: its arrivals were made before barrier
+             * 1's wait, so it is usually complete already and its poll round trip is skipped */
+            s_b2 = ldc<true>(b2);
         }
-        if (tid < 2) { s_bk[tid] = -1; s_bef[tid] = 0; s_bn[tid] = 0; }
     }
+    if (tid < 2) { s_bk[tid] = -1; s_bef[tid] = 0; s_bn[tid] = 0; }
     uint32_t cb8[BPT]; /* buckets BPT * tid .. + BPT - 1, every load in flight before any is used */
 #pragma unroll
-    for (int j = 0; j < BPT; ++j) cb8[j] = ldc<true>(st->sub + BPT * tid + j);
+    for (int j = 0; j < BPT; ++j) cb8[j] = solo ? lsub[BPT * tid + j] : ldc<true>(st->sub + BPT * tid + j);
     uint32_t cs = 0;
 #pragma unroll
     for (int j = 0; j < BPT; ++j) cs += cb8[j];
@@ -1582,18 +1616,32 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     uint32_t before = 0;
     int m = 0;
     uint32_t* stage = raw; /* the window histogram is done with */
+    const uint32_t* sel_keys = stage; /* the staged keys of the ranks' buckets */
     if (!full && (ca == 2 || cb == 2)) {
         const int ba = ca == 2 ? s_bk[0] : s_bk[1], bb = cb == 2 ? s_bk[1] : s_bk[0];
         before = ca == 2 ? s_bef[0] : s_bef[1];
         const uint32_t nlo = ca == 2 ? s_bn[0] : s_bn[1], nhi = (bb != ba) ? s_bn[1] : 0u;
         m = (int)(nlo + nhi);
-        if (m > RES_SEL_MAX) {
+        if (solo) {
+            /* the ranks' buckets ba..bb are one run of this workgroup's sorted keys in LDS (the
+             * buckets between are empty); pos[b] is the end of bucket b after the scatter */
+            sel_keys = srt + (ba ? pos[ba - 1] : 0u);
+            const uint32_t lo = (uint32_t)((uint64_t)kl + ((uint64_t)ba << sh));
+            const uint32_t hi = (uint32_t)min((uint64_t)kh, (uint64_t)kl + ((uint64_t)(bb + 1) << sh) - 1);
+            uint32_t xa = kl, xb = kl;
+            select_in_range<CT>([&](int64_t i) { return sel_keys[i]; }, [](uint32_t) { return true; }, (int64_t)m, lo,
+                                hi, ja - (int64_t)before, jb - (int64_t)before, ca == 2, cb == 2, &xa, &xb);
+            ka = ca == 2 ? xa : kl;
+            kb = cb == 2 ? xb : kl;
+            path = MODE_CAND;
+        } else if (m > RES_SEL_MAX) {
             full = true; /* uniform over the segment: the same totals everywhere */
         } else {
             /* ---- barrier 2: every region of the segment is published (its arrivals were made
              * before barrier 1's wait, so this wait is short) */
             WTP_PROBE(3);
-            if (!res_wait(b2, nwg, tmo)) {
+            const uint32_t b2v = s_b2; /* block-uniform */
+            if (!(b2v >= nwg && !(b2v & RES_POISON)) && !res_wait(b2, nwg, tmo)) {
                 if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
                 return;
             }
@@ -1690,7 +1738,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             } else {
                 uint32_t c = 0;
                 if (path == MODE_CAND)
-                    for (int i = tid; i < m; i += CT) c += stage[i] < tk;
+                    for (int i = tid; i < m; i += CT) c += sel_keys[i] < tk;
                 const unsigned long long sc = block_sum_u64<CT>(c);
                 zc = (unsigned long long)sbelow +
                      (path == MODE_CAND ? (unsigned long long)before : 0ull) + sc;

@@ -71,6 +71,7 @@ enum SegFlags : int32_t {
     SEG_ALIGNED = 2,   /* data (and out) 16-byte aligned: float4 path              */
     SEG_MINPRUNE = 4,  /* min-weight pruning: rank k-1 = r0 select, k_minmask writes */
     SEG_KZERO = 8,     /* min-weight pruning with k = 0: nothing pruned              */
+    SEG_LATE = 16,     /* k_resident: the late group (window first, then the chunk's loads) */
 };
 
 struct SegDesc {
@@ -185,6 +186,10 @@ static_assert(RES_SPL + RES_IT <= 63 && RES_SPL * 64 * RES_SW == RES_MS, "k_resi
  * scan of the segment, 4 sigma makes that ~1e-4 per segment; the three-launch form keeps 6 + 24 */
 constexpr int RES_SIGMA_X100 = 400;
 constexpr int RES_MAX_WG = 256;                     /* workgroups a resident launch may hold (<= CUs) */
+/* the late group: the smallest segments of a launch group, together at most this percentage of
+ * its workgroups; their workgroups issue their chunk's loads only once their window is known, so
+ * the early group's chunks come off HBM first and its select overlaps the late group's stream */
+constexpr int RES_LATE_PCT = 45;
 constexpr int RES_STG = 32;                         /* inside keys a thread may stage (of its 96; ~11 expected) */
 /* After the first segment barrier every workgroup publishes the keys of the (one or two)
  * buckets holding the segment's ranks in a slot of its own: word 0 the count, then the keys */
