@@ -130,6 +130,11 @@ def rocprof_child(args, timeout=240):
         subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                        timeout=timeout, check=True)
         stats = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+        keep = os.environ.get("WTP_BENCH_TRACE_DIR")  # lab: keep the child's trace and stats
+        if keep:
+            os.makedirs(keep, exist_ok=True)
+            for f in glob.glob(os.path.join(d, "**", "*kernel_*.csv"), recursive=True):
+                shutil.copy(f, os.path.join(keep, os.path.basename(f)))
         out = {}
         with open(stats[0]) as fh:
             for row in csv.DictReader(fh):

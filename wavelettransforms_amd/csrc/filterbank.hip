@@ -41,7 +41,11 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #define WTP_FB_INV_WPE __attribute__((amdgpu_waves_per_eu(5)))
 
 constexpr int FB_THREADS = 256;
-constexpr int FR = 16, FC = 64;  /* forward output tile (per subband) */
+/* forward output tile (per subband).  FC = 56: the axis -2 pass has 2 (2 FC + F - 2) column items,
+ * <= 256 for F <= 18, so every thread of the workgroup takes exactly one (with FC = 64 and db8,
+ * 284 items: wave 0 -- always on the same SIMD -- took a second one, doubling that SIMD's share
+ * of the pass; cfg5 forward levels -5 %) */
+constexpr int FR = 16, FC = 56;
 constexpr int IR = 64, IC = 64;  /* inverse output tile */
 constexpr int INV_RG = 2; /* synthesis row-pass rows interleaved per wave */
 constexpr int FB_MAX_LDS = 64 * 1024;
@@ -592,7 +596,9 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
     const float* rhi = tp.f[3];
     constexpr int HM = FT ? FT / 2 : 1;
     const int m = m0 + lane;
-    constexpr int RRN = (IR / 2 + HM + 2 + 3) / 4; /* rows per wave (NR_MAX / 4) */
+    /* rows per wave: a tile's coefficient rows NRr = r_hi - r_lo + 1 <= IR/2 + H (the sites of
+     * IR consecutive outputs span IR/2 positions; H even: exactly IR/2 + H) */
+    constexpr int RRN = (IR / 2 + HM + 3) / 4;
     f2 rowres[FT ? RRN : 1];
     if (lane < IC && m <= ml) {
         const SiteU s = site_u(m, a.C, F);
