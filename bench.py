@@ -447,6 +447,9 @@ def main():
         handles = (ctypes.c_void_p * len(sevs))(*[e.cuda_event for e in sevs])
         per_st = {st: [] for st in STAGES}
         L.wtp_set_stage_events(handles, len(sevs))
+        # the stage intervals need the stages in sequence on one stream: the selection pipeline
+        # (wtp_set_pipeline, several launch groups) is switched off for this leg only
+        pipe_prev = engine.set_pipeline(False)
         try:
             for _ in range(args.stage_reps):
                 torch.cuda._sleep(1_000_000)
@@ -456,6 +459,7 @@ def main():
                     per_st[st].append(sevs[i].elapsed_time(sevs[i + 1]) * 1e3)
         finally:
             L.wtp_set_stage_events(None, 0)
+            engine.set_pipeline(pipe_prev)
 
         work = None if args.flatten else dwt_stage_work(
             [(tuple(x.shape), r["eff_level"]) for x, r in zip(xs, recs)], int(L.wtp_dec_len(engine.wavelet_id(wavelet))))
@@ -472,8 +476,8 @@ def main():
         dom = max((st for st in ran if sbytes(st) > 0), key=lambda st: stage_us[st])
         dom_us, dom_bytes = stage_us[dom], sbytes(dom)
         dom_launches = max(r["eff_level"] for r in recs) if dom in DWT_STAGES else 1
-        timing_src = ("HIP events around the stage on the library's stream (median of %d calls; the interval "
-                      "includes dispatch gaps)" % args.stage_reps)
+        timing_src = ("HIP events around the stage on the library's stream (median of %d calls, selection "
+                      "pipeline off; the interval includes dispatch gaps)" % args.stage_reps)
     dom_kernel = dom if dom in ("k_resident", "k_small") else KERNEL_OF_STAGE.get(dom, dom)
     if dom_us is not None and dom_us > ms_per_step * 1e3 and world == 1:
         timing_src += "; capped at ms_per_step"

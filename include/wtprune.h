@@ -180,6 +180,13 @@ int wtp_resident_capacity(void); /* 0 if the current device cannot host the resi
  * ticks of the 100 MHz wall clock); tests lower it to force the fault path. */
 unsigned wtp_set_resident_timeout_us(unsigned us);
 #define WTP_PATH_FAULT 99
+/* A call with more than one launch group (24 tensors) of wavelet-transformed tensors runs each
+ * group's percentile selection on a side stream of the library's (one per device and caller
+ * stream, non-blocking, created on first use), overlapping the next group's forward transform;
+ * the caller's stream waits for it before that group's inverse, so the call stays ordered on
+ * the caller's stream (graph capture included).  Mode 0: everything on the caller's stream.
+ * Returns the previous mode (process-wide). */
+int wtp_set_pipeline(int mode);
 #define WTP_PATH_SMALL 4 /* every tensor of the call ran in one launch (2-D transforms, small population) */
 /* measurement hook (bench.py): while set, every resident launch atomically lowers stamps_dev[0] to
  * its first workgroup's start and raises stamps_dev[1] to its last workgroup's end (after that

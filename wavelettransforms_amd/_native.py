@@ -80,6 +80,7 @@ def lib():
             "wtp_random_prune_f32": ([tp, i32, ctypes.POINTER(i64), ctypes.c_uint64, vp, vp], i32),
             "wtp_count_small_f32": ([vp, i64, ctypes.c_float, vp, vp], i32),
             "wtp_set_resident": ([i32], i32),
+            "wtp_set_pipeline": ([i32], i32),
             "wtp_resident_capacity": ([], i32),
             "wtp_set_resident_timeout_us": ([ctypes.c_uint], ctypes.c_uint),
             "wtp_set_kernel_stamps": ([vp], i32),

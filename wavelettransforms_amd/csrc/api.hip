@@ -10,6 +10,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -27,6 +29,7 @@ thread_local int g_err_tensor = -1;
 thread_local hipEvent_t g_stage_ev[8];
 thread_local int g_stage_n = 0;
 std::atomic<int> g_resident{1}; /* wtp_set_resident */
+std::atomic<int> g_pipeline{1}; /* wtp_set_pipeline */
 
 inline void stage(int i, hipStream_t s) {
     if (i < g_stage_n && g_stage_ev[i]) (void)hipEventRecord(g_stage_ev[i], s);
@@ -557,6 +560,10 @@ int wtp_set_resident(int mode) {
     return prev;
 }
 int wtp_resident_capacity(void) { return resident_capacity(); }
+int wtp_set_pipeline(int mode) {
+    if (mode < 0 || mode > 1) return fail(WTP_EARG, -1, "bad pipeline mode %d", mode);
+    return g_pipeline.exchange(mode);
+}
 unsigned wtp_set_resident_timeout_us(unsigned us) { return set_resident_timeout_us(us); }
 int wtp_set_kernel_stamps(unsigned long long* stamps_dev) {
     set_kernel_stamps(stamps_dev);
@@ -577,6 +584,36 @@ int wtp_workspace_init(void* ws, size_t bytes, wtp_stream_t stream) {
     if (bytes && hipMemsetAsync(ws, 0, bytes, (hipStream_t)stream) != hipSuccess)
         return fail(WTP_EHIP, -1, "hipMemsetAsync failed");
     return WTP_OK;
+}
+
+/* The selection pipeline's side stream (one per device and caller stream, non-blocking, created
+ * on first use and kept) and its events: a call with several launch groups of DWT segments runs
+ * group g's forward levels on the caller's stream and its selection (window / collect /
+ * mask-select: HBM-bound) on the side stream, so it overlaps the next group's forward levels or
+ * the previous group's inverse levels (VALU-bound); the caller's stream waits for every group's
+ * selection before that group's inverse, which joins the side stream back (graph capture
+ * included).  Selections stay serialised on the side stream (the SelHeader parity regions). */
+struct SidePipe {
+    hipStream_t side = nullptr;
+    std::vector<hipEvent_t> ev;
+};
+std::mutex g_pipe_mu;
+std::map<std::pair<int, hipStream_t>, SidePipe> g_pipes;
+SidePipe* side_pipe(hipStream_t s, int nev) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    SidePipe& sp = g_pipes[{dev, s}];
+    if (!sp.side && hipStreamCreateWithFlags(&sp.side, hipStreamNonBlocking) != hipSuccess) {
+        sp.side = nullptr;
+        return nullptr;
+    }
+    while ((int)sp.ev.size() < nev) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        sp.ev.push_back(e);
+    }
+    return &sp;
 }
 
 static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, void* ws,
@@ -611,6 +648,8 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     }
     /* 1. forward transforms into the packed arrays (pywt.wavedec2 + coeffs_to_array) */
     std::vector<Chain> chains;
+    const int ngroups = (ntensors + SEG_PER_LAUNCH - 1) / SEG_PER_LAUNCH;
+    std::vector<std::vector<Chain>> gchains(ngroups);
     for (int t = 0; t < ntensors; ++t) {
         const TPlan& p = ps[t];
         if (!p.dwt) continue;
@@ -630,15 +669,26 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         c.thr = thr_t + t;
         c.zc = reinterpret_cast<unsigned long long*>(&results[t].zero_count);
         chains.push_back(c);
+        gchains[t / SEG_PER_LAUNCH].push_back(c);
         if (!p.tight && hipMemsetAsync(c.P, 0, (size_t)p.pop * sizeof(float), s) != hipSuccess)
             return fail(WTP_EHIP, t, "hipMemsetAsync failed");
     }
-    forward_chains(chains, tp, s);
+    int dwt_groups = 0;
+    for (const auto& gc : gchains) dwt_groups += !gc.empty();
+    SidePipe* pipe = (dwt_groups > 1 && g_pipeline.load(std::memory_order_relaxed)) ? side_pipe(s, 2 * ngroups) : nullptr;
+    const hipStream_t ss = pipe ? pipe->side : s; /* the selection's stream */
+    if (!pipe) forward_chains(chains, tp, s);
     /* 2. exact percentile selection + level-0 mask, SEG_PER_LAUNCH segments per launch group:
      * one resident launch when every segment of the group is level-0 and the group's chunks fit
      * the co-resident grid, else window / collect / mask-select */
     for (int g0 = 0; g0 < ntensors; g0 += SEG_PER_LAUNCH) {
         const int g1 = std::min(ntensors, g0 + SEG_PER_LAUNCH);
+        const int gi = g0 / SEG_PER_LAUNCH;
+        if (pipe) { /* this group's forward levels on the caller's stream, its selection behind them */
+            forward_chains(gchains[gi], tp, s);
+            if (hipEventRecord(pipe->ev[2 * gi], s) != hipSuccess || hipStreamWaitEvent(ss, pipe->ev[2 * gi], 0) != hipSuccess)
+                return fail(WTP_EHIP, -1, "hipEventRecord / hipStreamWaitEvent failed");
+        }
         bool all0 = true;
         int64_t rblk = 0;
         for (int t = g0; t < g1; ++t) {
@@ -692,24 +742,34 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         tab.nblk = blk;
         for (int i = tab.nseg; i < SEG_PER_LAUNCH; ++i) tab.blk_begin[i] = INT32_MAX;
         const bool first = g0 == 0;
-        if (first) stage(1, s);
+        if (first) stage(1, ss);
         if (resident) {
-            if (first) { stage(2, s); stage(3, s); }
-            launch_resident(tab, head, cand, results, thr_t, s);
+            if (first) { stage(2, ss); stage(3, ss); }
+            launch_resident(tab, head, cand, results, thr_t, ss);
         } else {
-            launch_window(tab, head, s);
-            if (first) stage(2, s);
-            launch_collect(tab, head, cand, results, s);
-            if (first) stage(3, s);
-            launch_mask_select(tab, head, cand, results, thr_t, s);
+            launch_window(tab, head, ss);
+            if (first) stage(2, ss);
+            launch_collect(tab, head, cand, results, ss);
+            if (first) stage(3, ss);
+            launch_mask_select(tab, head, cand, results, thr_t, ss);
             bool inplace = false;
             for (int i = 0; i < tab.nseg; ++i) inplace = inplace || (tab.s[i].out && tab.s[i].out == tab.s[i].data);
-            if (inplace) launch_mask_inplace(tab, results, thr_t, s);
+            if (inplace) launch_mask_inplace(tab, results, thr_t, ss);
         }
-        if (first) stage(4, s);
+        if (first) stage(4, ss);
+        if (pipe && hipEventRecord(pipe->ev[2 * gi + 1], ss) != hipSuccess)
+            return fail(WTP_EHIP, -1, "hipEventRecord failed");
     }
-    /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2) */
-    inverse_chains(chains, tp, s);
+    /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2); in
+     * the pipelined form group by group, each behind its selection (which joins the side stream) */
+    if (pipe) {
+        for (int gi = 0; gi < ngroups; ++gi) {
+            if (hipStreamWaitEvent(s, pipe->ev[2 * gi + 1], 0) != hipSuccess) return fail(WTP_EHIP, -1, "hipStreamWaitEvent failed");
+            inverse_chains(gchains[gi], tp, s);
+        }
+    } else {
+        inverse_chains(chains, tp, s);
+    }
     for (int t = 0; t < ntensors; ++t) {
         const TPlan& p = ps[t];
         if (!p.flat || !p.dwt) continue;

@@ -221,6 +221,12 @@ def set_resident(enabled):
     return bool(N.lib().wtp_set_resident(1 if enabled else 0))
 
 
+def set_pipeline(enabled):
+    """Overlap each launch group's selection with the next group's forward transform on a side
+    stream (include/wtprune.h wtp_set_pipeline); returns the previous setting."""
+    return bool(N.lib().wtp_set_pipeline(1 if enabled else 0))
+
+
 def resident_capacity():
     """Workgroups (of 49152 weights) the resident launch can hold on the current device; 0: never used."""
     return int(N.lib().wtp_resident_capacity())
