@@ -45,7 +45,9 @@ def _equal(a, b):
     (oa, ra), (ob, rb) = a, b
     for x, y, p, q in zip(oa, ob, ra, rb):
         assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
-        assert p["zero_count"] == q["zero_count"] and p["path"] == q["path"]
+        # path is a diagnostic: the window form a group takes (inline sample or k_window) depends on
+        # the group's size, so it may differ with the grouping; the results may not
+        assert p["zero_count"] == q["zero_count"] and p["eff_level"] == q["eff_level"]
         assert G.f64_bits_equal(p["thr64"], q["thr64"])
 
 
