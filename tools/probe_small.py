@@ -16,7 +16,8 @@ PROBE_LIB = os.path.join(ROOT, "tools", "mb", "libwtprune_probe.so")
 PHASES = [(6, "entry"), (0, "windows"), (1, "L0 loaded"), (10, "arrived 0"), (11, "barrier 0"),
           (2, "bin located"), (3, "slot written"), (4, "arrived 1"), (5, "barrier 1"), (7, "windows in LDS"),
           (8, "slots in LDS"), (9, "slot headers"), (12, "pass A"), (13, "ranks"), (14, "I start"),
-          (15, "stores drained")]
+          (15, "stores drained"), (16, "F1 axis-2"), (17, "F1 axis-1"), (18, "F2 axis-2"), (19, "F2 axis-1"),
+          (20, "F3 axis-2"), (21, "F3 axis-1"), (22, "I3 axis-1"), (24, "I2 axis-1"), (26, "I1 axis-1")]
 
 
 def build():
@@ -40,7 +41,7 @@ def main():
     spec = W.CONFIGS[cfg]
     ts = spec["tensors"]()
     xs = [eng.synth(s, seed, tid, e) for _, s, seed, tid, e in ts]
-    stamps = torch.zeros(2 + 16 * 256, dtype=torch.int64, device="cuda")
+    stamps = torch.zeros(2 + 32 * 256, dtype=torch.int64, device="cuda")
     L = N.lib()
     runs = []
     warm = os.environ.get("PROBE_WARM")  # stamp the second of two back-to-back launches
@@ -60,10 +61,10 @@ def main():
         L.wtp_set_kernel_stamps(None)
         s = stamps.cpu().numpy()
         t0 = s[0]
-        blk = s[2:].reshape(256, 16)
+        blk = s[2:].reshape(256, 32)
         used = blk[:, 0] > 0
         if it >= 10:
-            runs.append(((blk[used, :16] - t0) * 0.01, (s[1] - t0) * 0.01))
+            runs.append(((blk[used, :32] - t0) * 0.01, (s[1] - t0) * 0.01))
     res = eng.decode(resd, len(xs))
     for (name, s, seed, tid, e), o, r in zip(ts, outs, res):
         ref, rr = O.prune_tensor(W.synth_numpy(s, seed, tid, e), spec["wavelet"], spec["level"], spec["pct"])

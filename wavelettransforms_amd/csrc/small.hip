@@ -34,11 +34,11 @@ static_assert(SM_MAX_L == wtp::SM_LMAX, "level bound");
 
 namespace wtp {
 
-/* phase stamps for tools/probe_small.py (a -DWTP_SM_PROBE build only): stamps[2 + 16 b + i] */
+/* phase stamps for tools/probe_small.py (a -DWTP_SM_PROBE build only): stamps[2 + 32 b + i] */
 #ifdef WTP_SM_PROBE
 #define SM_PROBE(i) \
     do { \
-        if (t.stamps && threadIdx.x == 0) t.stamps[2 + 16 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if (t.stamps && threadIdx.x == 0) t.stamps[2 + 32 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define SM_PROBE(i)
@@ -430,6 +430,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                 LH[e] = make_float2(a, d);
             }
             __syncthreads();
+            if (k <= 3) SM_PROBE(14 + 2 * k); /* 16, 18, 20: level k's axis -2 pass */
         }
         /* axis -1: aa, ad from the L rows, da, dd from the H rows; aa is the next level's input */
         {
@@ -499,6 +500,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
             kbase += (3 + last) * plane;
         }
         __syncthreads();
+        if (k <= 3) SM_PROBE(15 + 2 * k); /* 17, 19, 21: level k's axis -1 pass */
     }
     /* the packed array's padding (non-tight layouts) holds zeros: keys 0, counted by tile 0 */
     const uint32_t npad = lt == 0 ? (uint32_t)g.npad : 0u;
@@ -867,6 +869,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
             }
         }
         __syncthreads();
+        if (L - k <= 2) SM_PROBE(22 + 2 * (L - k)); /* 22, 24, 26: synthesis level k's axis -1 pass */
         /* axis -2: y = rec_lo over lo, then rec_hi over hi, at the output rows orr */
         {
             const int n = orr.len * oc.len;
