@@ -633,11 +633,16 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
                         acc[gq] = f2{0.0f, 0.0f};
                         rb[gq] = min(wv + 4 * min(q0 + gq, RRN - 1), NRr - 1) * NCc + s.iu - c_lo;
                     }
+                    /* each row's HM samples from ONE base address (the lowest), so the reads take
+                     * immediate offsets (ds_read2_b64 offset0 / offset1) instead of an address each */
+                    const float2* pa[G];
+#pragma unroll
+                    for (int gq = 0; gq < G; ++gq) pa[gq] = Aq + (rb[gq] - (HM - 1));
 #pragma unroll
                     for (int gq = 0; gq < G; ++gq)
 #pragma unroll
                         for (int j = 0; j < HM; ++j) {
-                            const float2 t = Aq[rb[gq] - j];
+                            const float2 t = pa[gq][HM - 1 - j];
                             v[gq][j] = f2{t.x, t.y};
                         }
 #pragma unroll
@@ -649,7 +654,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
                     for (int gq = 0; gq < G; ++gq)
 #pragma unroll
                         for (int j = 0; j < HM; ++j) {
-                            const float2 t = Dq[rb[gq] - j];
+                            const float2 t = (pa[gq] + (Dq - Aq))[HM - 1 - j];
                             v[gq][j] = f2{t.x, t.y};
                         }
 #pragma unroll
