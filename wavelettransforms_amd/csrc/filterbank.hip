@@ -547,7 +547,9 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
     /* 1. the four coefficient tiles (periodic wrap, thresholded on load); all loads of a
      *    thread issued before the LDS writes (compile-time trip count) */
     {
-        constexpr int NR_MAX = IR / 2 + (FT ? FT : 2) / 2 + 2, NC_MAX = IC / 2 + (FT ? FT : 2) / 2 + 2;
+        /* a tile's coefficient rows / columns: NRr <= IR/2 + H, NCc <= IC/2 + H (its IR outputs sit on
+         * IR/2 consecutive synthesis sites; the H-even special last output n = 2N - 1 included) */
+        constexpr int NR_MAX = IR / 2 + (FT ? FT : 2) / 2, NC_MAX = IC / 2 + (FT ? FT : 2) / 2;
         const bool inner = r_lo >= 0 && r_hi < a.R && c_lo >= 0 && c_hi < a.C;
         auto load4 = [&](int rr, int cc, float4& q) {
             const int r = inner ? r_lo + rr : pmod32(r_lo + rr, a.R), c = inner ? c_lo + cc : pmod32(c_lo + cc, a.C);
@@ -796,7 +798,9 @@ static size_t fwd_lds(int F, bool alias = false) {
     return sizeof(float) * (alias ? std::max(t, lh) : t + lh);
 }
 static size_t inv_lds(int F, bool alias = false) {
-    const size_t nr = IR / 2 + F / 2 + 2, nc = IC / 2 + F / 2 + 2;
+    /* the tile bounds of k_inv_level (IR/2 + H rows, IC/2 + H columns): db8 40 x 40, 25.6 KB aliased --
+     * six workgroups per CU instead of five */
+    const size_t nr = IR / 2 + F / 2, nc = IC / 2 + F / 2;
     return sizeof(float) * (alias ? std::max(4 * nr * nc, 2 * nr * IC) : 4 * nr * nc + 2 * nr * IC);
 }
 
