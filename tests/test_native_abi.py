@@ -89,3 +89,16 @@ def test_workspace_size_covers_both_level_modes():
     d = _desc([(4, 4, 3, 3), (2, 64, 64)])
     wid = L.wtp_wavelet_id(b"haar")
     assert L.wtp_workspace_size(d, 2, wid, 5) >= L.wtp_workspace_size(_desc([(2, 64, 64)]), 1, wid, 5)
+
+
+def test_mode_switches_validate_and_return_the_previous_mode():
+    """wtp_set_resident / wtp_set_pipeline: 0 or 1, the previous mode returned, anything else
+    rejected with WTP_EARG and the mode left as it was (host logic only, no device work)."""
+    L = N.lib()
+    for setter in (L.wtp_set_resident, L.wtp_set_pipeline):
+        prev = setter(0)
+        assert prev in (0, 1)
+        assert setter(1) == 0
+        assert setter(2) < 0 and setter(-1) < 0
+        assert setter(1) == 1  # unchanged by the rejected calls
+        setter(prev)
