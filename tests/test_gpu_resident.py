@@ -287,3 +287,21 @@ def test_nan_and_inf_in_either_half(eng, mode):
         assert np.array_equal(o.cpu().numpy(), ref, equal_nan=True)
         assert r["zero_count"] == rr["zero_count"]
         assert G.f64_bits_equal(r["thr64"], rr["thr64"]) or (np.isnan(r["thr64"]) and np.isnan(rr["thr64"]))
+
+
+@pytest.mark.parametrize("n", [4000, 40_000, RES_CHUNK])
+def test_solo_overflow_then_reuse(eng, n):
+    """A one-workgroup segment whose staging columns overflow (a zero-heavy / constant tensor:
+    every key inside the window) takes the full scan; the parity flip of that launch must leave
+    the workspace clean, so the calls after it on the same workspace stay exact."""
+    rng = np.random.default_rng(n)
+    z = np.zeros(n, np.float32)
+    z[rng.integers(0, n, n // 20)] = (rng.standard_normal(n // 20) * 0.05).astype(np.float32)
+    c = np.full(n, -0.125, np.float32)
+    normal = (rng.standard_normal(300_000) * 0.05).astype(np.float32)
+    for _ in range(3):
+        for x in (z, c, normal, z):
+            outs, (r,) = eng.prune([_dev(x)], "haar", 0, 50.0)
+            ref, rr = O.prune_tensor(x.copy(), "haar", 0, 50.0)
+            _same(outs[0].cpu().numpy(), ref, r, rr)
+            assert r["path"] != eng.MODE_FAULT

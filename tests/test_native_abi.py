@@ -102,3 +102,17 @@ def test_mode_switches_validate_and_return_the_previous_mode():
         assert setter(2) < 0 and setter(-1) < 0
         assert setter(1) == 1  # unchanged by the rejected calls
         setter(prev)
+
+
+def test_integration_stub_is_the_documented_block():
+    """INTEGRATION.md section 2's code block is exactly tests/integration_stub.py's body (the GPU
+    suite runs that file: tests/test_gpu_integration_stub.py)."""
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    i = doc.index("```python\nimport ctypes, torch") + len("```python\n")
+    block = doc[i:doc.index("```\n", i)]
+    src = open(os.path.join(root, "tests", "integration_stub.py")).read()
+    a = src.index("# --- begin INTEGRATION.md block ---\n") + len("# --- begin INTEGRATION.md block ---\n")
+    body = src[a:src.index("# --- end INTEGRATION.md block ---")]
+    assert body == block

@@ -57,12 +57,17 @@ def _oracle_prune(wavelet, level, pct):
     return fn
 
 
-def _worker(rank, world, port, q):
+def _tensors(ntens):
+    ts = W.resnet18_tensors(0)[:7] + [("mlp", (10, 128), 101, 1, 14)]
+    return ts if ntens is None else ts[:ntens]
+
+
+def _worker(rank, world, port, q, ntens=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        ts = W.resnet18_tensors(0)[:7] + [("mlp", (10, 128), 101, 1, 14)]
+        ts = _tensors(ntens)
         xs = [torch.from_numpy(W.synth_numpy(s, seed, tid, e)) for _, s, seed, tid, e in ts]
         full, recs, plan = prune_sharded(xs, "haar", 2, 61.8, _oracle_prune("haar", 2, 61.8),
                                          device=torch.device("cpu"))
@@ -77,14 +82,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.timeout(300)
-def test_prune_sharded_gloo_world2():
-    from oracle import oracle as O
-    world = 2
+def _run_world(world, ntens=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, ntens)) for r in range(world)]
     for p in procs:
         p.start()
     import queue
@@ -97,7 +99,15 @@ def test_prune_sharded_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ts = W.resnet18_tensors(0)[:7] + [("mlp", (10, 128), 101, 1, 14)]
+    return got
+
+
+@pytest.mark.timeout(300)
+def test_prune_sharded_gloo_world2():
+    from oracle import oracle as O
+    world = 2
+    got = _run_world(world)
+    ts = _tensors(None)
     refs = [O.prune_tensor(W.synth_numpy(s, seed, tid, e), "haar", 2, 61.8) for _, s, seed, tid, e in ts]
     mines = [g[3] for g in got]
     assert all(m == mines[0] for m in mines) and all(mines[0])  # both ranks own layers
@@ -106,3 +116,19 @@ def test_prune_sharded_gloo_world2():
             assert np.array_equal(f, ref)
             assert r["zero_count"] == rr["zero_count"] and r["eff_level"] == rr["eff_level"]
             assert np.float64(r["thr64"]).tobytes() == np.float64(rr["thr64"]).tobytes()
+
+
+@pytest.mark.timeout(300)
+def test_prune_sharded_gloo_more_ranks_than_tensors():
+    """world 3 over 2 tensors: one rank owns nothing, its region is empty and no zero-element
+    point-to-point operation is posted for it; every rank still ends with the whole result"""
+    from oracle import oracle as O
+    got = _run_world(3, ntens=2)
+    ts = _tensors(2)
+    refs = [O.prune_tensor(W.synth_numpy(s, seed, tid, e), "haar", 2, 61.8) for _, s, seed, tid, e in ts]
+    mines = got[0][3]
+    assert sum(1 for m in mines if not m) == 1
+    for rank, full, recs, _ in got:
+        for (ref, rr), f, r in zip(refs, full, recs):
+            assert np.array_equal(f, ref)
+            assert r["zero_count"] == rr["zero_count"]

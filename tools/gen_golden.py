@@ -265,6 +265,7 @@ def main():
     large("cfg2_haar_L5", "haar", 5, [50.0], W.resnet18_tensors(0))
     large("cfg3_rbio22_L3", "rbio2.2", 3, [50.0, 90.0], W.mlp_tensors(3))
     large("cfg5_db8_L5_block0", "db8", 5, [50.0], W.block_tensors(1))
+    large_cfg5_groups(manifest)
     large("b1024_db8_L5", "db8", 5, [50.0, 75.0], W.block_tensors(2, side=1024, seed=6))
 
     np.savez_compressed(os.path.join(OUT, "cases.npz"), **arrays)
@@ -273,5 +274,29 @@ def main():
     print("golden fixtures written in %.1fs" % (time.time() - t0), file=sys.stderr)
 
 
+CFG5_GROUP_BLOCKS = [0, 23, 24, 47, 48, 63]  # the first and last block of each 24/24/16 launch group
+
+
+def large_cfg5_groups(manifest):
+    """cfg5 exactly as bench.py runs it (64 blocks of 4096^2, db8 L5, p50, one call): one block from
+    each end of every launch group, their index in the 64-block list recorded."""
+    out = []
+    blocks = W.block_tensors(64)
+    for i in CFG5_GROUP_BLOCKS:
+        name, shape, seed, tid, e = blocks[i]
+        rec, _, _, _ = mra_restated(W.synth_numpy(shape, seed, tid, e), "db8", 5, 50.0)
+        rec.update({"name": name, "synth": [seed, tid, e], "index": i})
+        out.append(rec)
+    manifest["large"]["cfg5_db8_L5_groups"] = out
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--cfg5-groups"]:  # add that record set to the committed manifest only
+        path = os.path.join(OUT, "manifest.json")
+        with open(path) as fh:
+            m = json.load(fh)
+        large_cfg5_groups(m)
+        with open(path, "w") as fh:
+            json.dump(m, fh, indent=1, sort_keys=True)
+    else:
+        main()

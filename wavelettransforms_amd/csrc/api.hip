@@ -600,8 +600,11 @@ struct SidePipe {
 std::mutex g_pipe_mu;
 std::map<std::pair<int, hipStream_t>, SidePipe> g_pipes;
 SidePipe* side_pipe(hipStream_t s, int nev) {
-    int dev = 0;
+    /* the side stream must live on the caller's stream's device: when that is not the current
+     * device (the caller set no device guard) the call keeps the single-stream form */
+    int dev = 0, sdev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (hipStreamGetDevice(s, &sdev) != hipSuccess || sdev != dev) return nullptr;
     std::lock_guard<std::mutex> lk(g_pipe_mu);
     SidePipe& sp = g_pipes[{dev, s}];
     if (!sp.side && hipStreamCreateWithFlags(&sp.side, hipStreamNonBlocking) != hipSuccess) {
@@ -675,8 +678,18 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     }
     int dwt_groups = 0;
     for (const auto& gc : gchains) dwt_groups += !gc.empty();
-    SidePipe* pipe = (dwt_groups > 1 && g_pipeline.load(std::memory_order_relaxed)) ? side_pipe(s, 2 * ngroups) : nullptr;
+    SidePipe* pipe = (dwt_groups > 1 && g_pipeline.load(std::memory_order_relaxed)) ? side_pipe(s, 2 * ngroups + 1) : nullptr;
     const hipStream_t ss = pipe ? pipe->side : s; /* the selection's stream */
+    /* an error after the first fork still joins the side stream back into the caller's (an
+     * unjoined fork invalidates a capture, and eagerly the caller may free what it still reads) */
+    bool forked = false;
+    auto fail_joined = [&](int t, const char* msg) {
+        if (forked) {
+            (void)hipEventRecord(pipe->ev[2 * ngroups], ss);
+            (void)hipStreamWaitEvent(s, pipe->ev[2 * ngroups], 0);
+        }
+        return fail(WTP_EHIP, t, "%s", msg);
+    };
     if (!pipe) forward_chains(chains, tp, s);
     /* 2. exact percentile selection + level-0 mask, SEG_PER_LAUNCH segments per launch group:
      * one resident launch when every segment of the group is level-0 and the group's chunks fit
@@ -686,8 +699,10 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         const int gi = g0 / SEG_PER_LAUNCH;
         if (pipe) { /* this group's forward levels on the caller's stream, its selection behind them */
             forward_chains(gchains[gi], tp, s);
-            if (hipEventRecord(pipe->ev[2 * gi], s) != hipSuccess || hipStreamWaitEvent(ss, pipe->ev[2 * gi], 0) != hipSuccess)
-                return fail(WTP_EHIP, -1, "hipEventRecord / hipStreamWaitEvent failed");
+            if (hipEventRecord(pipe->ev[2 * gi], s) != hipSuccess) return fail_joined(-1, "hipEventRecord failed");
+            if (hipStreamWaitEvent(ss, pipe->ev[2 * gi], 0) != hipSuccess)
+                return fail_joined(-1, "hipStreamWaitEvent failed");
+            forked = true;
         }
         bool all0 = true;
         int64_t rblk = 0;
@@ -757,14 +772,13 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             if (inplace) launch_mask_inplace(tab, results, thr_t, ss);
         }
         if (first) stage(4, ss);
-        if (pipe && hipEventRecord(pipe->ev[2 * gi + 1], ss) != hipSuccess)
-            return fail(WTP_EHIP, -1, "hipEventRecord failed");
+        if (pipe && hipEventRecord(pipe->ev[2 * gi + 1], ss) != hipSuccess) return fail_joined(-1, "hipEventRecord failed");
     }
     /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2); in
      * the pipelined form group by group, each behind its selection (which joins the side stream) */
     if (pipe) {
         for (int gi = 0; gi < ngroups; ++gi) {
-            if (hipStreamWaitEvent(s, pipe->ev[2 * gi + 1], 0) != hipSuccess) return fail(WTP_EHIP, -1, "hipStreamWaitEvent failed");
+            if (hipStreamWaitEvent(s, pipe->ev[2 * gi + 1], 0) != hipSuccess) return fail_joined(-1, "hipStreamWaitEvent failed");
             inverse_chains(gchains[gi], tp, s);
         }
     } else {

@@ -1474,6 +1474,10 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     }
     WTP_RPROBE(9);
     if (solo) {
+        /* s_arr (wave 7's store after its returning add) must be visible to wave 6: on the
+         * non-overflow path the publication's barriers order it; an overflowing solo segment has
+         * none of them (block-uniform branch) */
+        if (ovf) __syncthreads();
         /* the parity flip's second level (as the storing waves do it below) */
         if (tid == 64 * (NW - 2)) {
             const uint32_t sh8 = blockIdx.x & (NSHARD - 1);

@@ -143,8 +143,14 @@ def exchange(full, plan, rank, group=None):
             continue
         peer = dist.get_global_rank(group, p) if group is not None else p
         c0, c1 = plan.region(p)
-        ops.append(dist.P2POp(dist.isend, mine, peer, group))
-        ops.append(dist.P2POp(dist.irecv, full[c0:c1], peer, group))
+        # a rank that owns no tensor (world > number of layers) has an empty region: both sides
+        # read that from the shared plan and post no operation for it
+        if b1 > b0:
+            ops.append(dist.P2POp(dist.isend, mine, peer, group))
+        if c1 > c0:
+            ops.append(dist.P2POp(dist.irecv, full[c0:c1], peer, group))
+    if not ops:
+        return
     for req in dist.batch_isend_irecv(ops):
         req.wait()
 
