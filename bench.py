@@ -36,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 153.0  # one xGMI peer link, per direction (MI355X: 7 links per GPU)
 # FP32 vector rate without FMA contraction, mul + add counted as two flops: MEASURED on MI355X with
 # independent v_pk_mul_f32 / v_pk_add_f32 chains at >= 2 waves per SIMD (tools/mb/pkrate.hip,
 # profiles/r03_valu_nofma_rate.txt: 128 TF/s packed, 120 TF/s scalar); SURVEY.md 8(d)'s 78.6 was
@@ -70,6 +71,8 @@ def parse():
                     help="the 1-D flattened mode (WTP_FLATTEN; an extension, not the headline path)")
     ap.add_argument("--no-resident", action="store_true",
                     help="level-0 groups in the three-launch form instead of the one-launch k_resident")
+    ap.add_argument("--no-interior", action="store_true",
+                    help="run every filter-bank tile in the general kernel (wtp_set_interior(0); A/B only)")
     ap.add_argument("--no-rocprof", action="store_true", help="skip the in-run rocprofv3 kernel-stats child")
     ap.add_argument("--profile-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
@@ -125,6 +128,8 @@ def rocprof_child(args, timeout=240):
         cmd.append("--flatten")
     if args.no_resident:
         cmd.append("--no-resident")
+    if args.no_interior:
+        cmd.append("--no-interior")
     env = dict(os.environ, TMPDIR="/tmp")
     try:
         subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
@@ -246,6 +251,8 @@ def main():
     L = N.lib()
     if args.no_resident:
         engine.set_resident(False)
+    if args.no_interior:
+        engine.set_interior(False)
 
     # ---------------------------------------------------------------- workload
     if args.config == "cfg2":
@@ -539,6 +546,13 @@ def main():
                                     "bytes_sent_this_rank": plan.bytes_sent(rank),
                                     "bytes_received_this_rank": plan.bytes_received(rank),
                                     "bytes_received_max_rank": max(plan.bytes_received(r) for r in range(world)),
+                                    "largest_region_bytes": 4 * max(plan.size),
+                                    "per_link_estimate_us": 4 * max(plan.size) / XGMI_LINK_GBS / 1e3,
+                                    "exchange_status": "batch_isend_irecv over RCCL at N > 1 had not run on hardware "
+                                                       "before this line (covered by world-2/3 gloo and a world-1 "
+                                                       "RCCL group); per_link_estimate_us assumes every peer pair on "
+                                                       "its own xGMI link at %.0f GB/s, the largest region the "
+                                                       "longest copy" % XGMI_LINK_GBS,
                                     "note": "LPT layer shards pruned in place into the flat state_dict buffer, then "
                                             "ONE full-mesh exchange of the unpadded regions (weights + records; "
                                             "batch_isend_irecv = one RCCL group of point-to-point copies, one per "

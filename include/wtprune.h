@@ -187,6 +187,11 @@ unsigned wtp_set_resident_timeout_us(unsigned us);
  * the caller's stream (graph capture included).  Mode 0: everything on the caller's stream.
  * Returns the previous mode (process-wide). */
 int wtp_set_pipeline(int mode);
+/* The filter-bank levels run their interior tiles (input window inside the image, full tile)
+ * in kernels compiled without the edge forms, and the frame of edge tiles in the general
+ * kernel; mode 0 runs every tile in the general kernel (identical results).  Returns the
+ * previous mode (process-wide). */
+int wtp_set_interior(int mode);
 #define WTP_PATH_SMALL 4 /* every tensor of the call ran in one launch (2-D transforms, small population) */
 /* measurement hook (bench.py): while set, every resident launch atomically lowers stamps_dev[0] to
  * its first workgroup's start and raises stamps_dev[1] to its last workgroup's end (after that

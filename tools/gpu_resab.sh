@@ -1,6 +1,6 @@
 #!/bin/bash
 # k_resident A/B: resident parity tests + phase lab on the in-tree library, then cfg2 bench lines
-# alternating the in-tree library and tools/mb/libwtprune_base.so (HEAD before the change).
+# alternating the in-tree library and tools/ab/libwtprune_base.so (tools/build_base.sh: HEAD before the change).
 # Usage: gpurun --timeout 900 -- bash tools/gpu_resab.sh TAG
 set -o pipefail
 TAG=${1:-ab}
@@ -15,7 +15,7 @@ echo "== reslab"
 timeout -k 10 120 ./tools/mb/reslab 50 $OUT/reslab_$TAG.csv > $OUT/reslab_$TAG.log 2>&1 || { echo reslab failed; tail -20 $OUT/reslab_$TAG.log; exit 1; }
 grep -v "184466" $OUT/reslab_$TAG.log
 for v in new base new base; do
-  L=""; [ $v = base ] && L=$(pwd)/tools/mb/libwtprune_base.so
+  L=""; [ $v = base ] && L=$(pwd)/tools/ab/libwtprune_base.so
   WTP_LIB_PATH=$L timeout -k 10 300 python bench.py --no-cpu --no-cold > $OUT/b_${TAG}_$v.log 2>&1 || { tail -20 $OUT/b_${TAG}_$v.log; exit 1; }
   python3 -c "
 import json

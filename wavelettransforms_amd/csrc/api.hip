@@ -560,6 +560,8 @@ int wtp_set_resident(int mode) {
     return prev;
 }
 int wtp_resident_capacity(void) { return resident_capacity(); }
+int wtp_set_interior(int mode) { return fb_set_interior(mode); }
+
 int wtp_set_pipeline(int mode) {
     if (mode < 0 || mode > 1) return fail(WTP_EARG, -1, "bad pipeline mode %d", mode);
     return g_pipeline.exchange(mode);
@@ -750,7 +752,11 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             sd.cand_off = (int64_t)p.cand_off;
             sd.cap = p.cap;
             bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap, p.dwt);
-            if (resident) sd.nsub_log2 = RES_NSUB_LOG2;
+            if (resident) {
+                sd.nsub_log2 = RES_NSUB_LOG2;
+                if (p.pop > RES_MS)
+                    sd.res_step_fx = ((uint64_t)(p.pop - SAMPLE_GROUP) << 32) / (uint64_t)(RES_MS / SAMPLE_GROUP - 1);
+            }
             if (late[t - g0]) sd.flags |= SEG_LATE;
             blk += (int)((p.pop + chunk - 1) / chunk);
         }

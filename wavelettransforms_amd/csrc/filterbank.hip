@@ -21,6 +21,7 @@
 #include "wt_dwt_core.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -265,6 +266,9 @@ struct FwdArgs {
     float* anext;        /* (B, Ro, Co) next-level approximation; unused when last */
     int last, tilesC, tilesR;
     int al16;            /* in is 16-byte aligned and C % 4 == 0: interior tiles load float4 rows */
+    /* the interior tiles (k_fwd_int): rows tr0 .. tr0 + nTR - 1, columns tc0 .. tc0 + nTC - 1 of
+     * the tile grid; frame != 0: k_fwd_level runs only the tiles around that rectangle */
+    int tr0, nTR, tc0, nTC, frame;
 };
 
 /* One launch covers the same level of up to FB_UNI items of the SAME geometry (same filter; the
@@ -280,6 +284,35 @@ struct FwdGroup {
     float* P[FB_UNI];
 };
 template <int FT> using TapsT = typename std::conditional<FT == 0, Taps, SmallTaps>::type;
+
+/* frame index f -> tile (tr, tc) of a grid of tilesC columns around the interior rectangle
+ * [r0, r0 + nr) x [c0, c0 + nc): the rows above it, then the side tiles of its rows, then the
+ * rows below it (row-major inside each part) */
+__device__ __forceinline__ void frame_tile(int f, int tilesC, int r0, int nr, int c0, int nc, int* tr, int* tc) {
+    const int top = r0 * tilesC, side = tilesC - nc;
+    if (f < top) {
+        *tr = f / tilesC;
+        *tc = f - *tr * tilesC;
+        return;
+    }
+    f -= top;
+    if (f < nr * side) {
+        const int q = f / side, k = f - q * side;
+        *tr = r0 + q;
+        *tc = k < c0 ? k : k + nc;
+        return;
+    }
+    f -= nr * side;
+    *tr = r0 + nr + f / tilesC;
+    *tc = f - (f / tilesC) * tilesC;
+}
+
+/* taps of the interior kernels: analysis {dec_lo[j], dec_hi[j]} adjacent, so one SGPR pair is
+ * both bands' packed tap */
+struct FwdIntTaps {
+    f2 t[SM_F_MAX];
+};
+#define WTP_FB_INT_WPE __attribute__((amdgpu_waves_per_eu(6)))
 
 template <int FT>
 __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGroup g, TapsT<FT> tp) {
@@ -300,7 +333,16 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
     a.anext = g.anext[item];
     a.P = g.P[item];
     const int tile = gt - item * g.tiles;
-    const int tc = tile % a.tilesC, tr = (tile / a.tilesC) % a.tilesR, b = tile / (a.tilesC * a.tilesR);
+    int tc, tr, b;
+    if (a.frame) {
+        const int per = a.tilesR * a.tilesC - a.nTR * a.nTC;
+        b = tile / per;
+        frame_tile(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, &tr, &tc);
+    } else {
+        tc = tile % a.tilesC;
+        tr = (tile / a.tilesC) % a.tilesR;
+        b = tile / (a.tilesC * a.tilesR);
+    }
     const int o0r = tr * FR, o0c = tc * FC;
     const int gr0 = 2 * o0r - F / 2 + 1, gc0 = 2 * o0c - F / 2 + 1;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -484,6 +526,138 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
     WTP_FPROBE(3);
 }
 
+/* One analysis level over the INTERIOR tiles of a group (FwdGroup geo: tr0/nTR/tc0/nTC): every
+ * tile's input window lies inside the image and its float4 rows are aligned, every output is a
+ * full-tile interior site (i < N: ascending taps), so none of k_fwd_level's edge forms is compiled
+ * in -- the frame of edge tiles runs k_fwd_level.  Same sums in the same order (pywt's
+ * ascending-tap interior form, every sum from 0 as pywt starts it, so even the sign of a zero
+ * matches).  Instruction shape:
+ *   column pass: a thread's column samples are read as PAIRS of consecutive rows into aligned
+ *   register pairs, so the packed multiply broadcasts either sample by op_sel (no realigning
+ *   move), against the {lo[j], hi[j]} tap pair in one SGPR pair;
+ *   row pass: as k_fwd_level's interior form; stores by buffer instructions whose row offset is a
+ *   scalar (the row is wave-uniform) and column offset the lane's -- no 64-bit address math. */
+template <int FT>
+__global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup g, FwdIntTaps tp) {
+    static_assert(FT > 0 && FT % 2 == 0, "specialised even filters");
+    extern __shared__ float lds[];
+    constexpr int NRc = 2 * FR + FT - 2, NCc = 2 * FC + FT - 2;
+    constexpr int S0 = FWD_S0<FT>, TP = FWD_TP<FT>, W4 = TP / 4;
+    constexpr int HALF = (NCc + 1) / 2;
+    float* T = lds;
+    float2* LH = reinterpret_cast<float2*>(lds);
+    const int gt = xcd_tile(blockIdx.x, gridDim.x);
+    const int item = gt / g.tiles;
+    const FwdArgs& a = g.geo;
+    const int tile = gt - item * g.tiles;
+    const int per = a.nTR * a.nTC;
+    const int b = tile / per, t2 = tile - b * per;
+    const int trr = t2 / a.nTC;
+    const int o0r = (a.tr0 + trr) * FR, o0c = (a.tc0 + t2 - trr * a.nTC) * FC;
+    const int gr0 = 2 * o0r - FT / 2 + 1, gc0 = 2 * o0c - FT / 2 + 1;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const float* x = g.in[item] + (int64_t)b * a.in_bs;
+    WTP_FPROBE(0);
+    /* 1. the input tile, whole float4 rows from the aligned column gc0 - S0; every load of a
+     *    thread in flight before its first LDS write */
+    {
+        constexpr int NE = NRc * W4, K = (NE + FB_THREADS - 1) / FB_THREADS;
+        const float* x0 = x + (int64_t)gr0 * a.C + (gc0 - S0);
+        float4 q[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int e = min(k * FB_THREADS + (int)threadIdx.x, NE - 1);
+            const int rr = e / W4, j4 = e - rr * W4;
+            q[k] = *reinterpret_cast<const float4*>(x0 + (int64_t)rr * a.C + 4 * j4);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            reinterpret_cast<float4*>(T)[min(k * FB_THREADS + (int)threadIdx.x, NE - 1)] = q[k];
+    }
+    __syncthreads();
+    WTP_FPROBE(1);
+    /* 2. axis -2: one tile column and FR/2 consecutive output rows per item */
+    constexpr int RH = FR / 2, NV = 2 * RH + FT - 2, NP = NV / 2;
+    constexpr int NIT = (2 * NCc + FB_THREADS - 1) / FB_THREADS;
+    static_assert(NV % 2 == 0, "sample pairs");
+    f2 res[NIT][RH];
+#pragma unroll
+    for (int q = 0; q < NIT; ++q) {
+        const int it = threadIdx.x + q * FB_THREADS;
+        if (it < 2 * NCc) {
+            const int h = it >= NCc, cc = it - h * NCc;
+            const float* col = T + (2 * RH * h) * TP + S0 + cc;
+            f2 P[NP];
+#pragma unroll
+            for (int m = 0; m < NP; ++m) P[m] = f2{col[(2 * m) * TP], col[(2 * m + 1) * TP]};
+            auto smp = [&](int s) { return (s & 1) ? P[s >> 1].yy : P[s >> 1].xx; };
+#pragma unroll
+            for (int r = 0; r < RH; ++r) res[q][r] = f2{0.0f, 0.0f} + tp.t[0] * smp(2 * r + FT - 1);
+#pragma unroll
+            for (int j = 1; j < FT; ++j)
+#pragma unroll
+                for (int r = 0; r < RH; ++r) res[q][r] = res[q][r] + tp.t[j] * smp(2 * r + FT - 1 - j);
+        }
+    }
+    __syncthreads(); /* every read of T is done: LH overwrites it */
+    auto lhi = [&](int o, int cc) { return o * NCc + (cc & 1) * HALF + (cc >> 1); };
+#pragma unroll
+    for (int q = 0; q < NIT; ++q) {
+        const int it = threadIdx.x + q * FB_THREADS;
+        if (it < 2 * NCc) {
+            const int h = it >= NCc, cc = it - h * NCc;
+#pragma unroll
+            for (int r = 0; r < RH; ++r) LH[lhi(RH * h + r, cc)] = make_float2(res[q][r].x, res[q][r].y);
+        }
+    }
+    __syncthreads();
+    WTP_FPROBE(2);
+    /* 3. axis -1 of the L and H rows -> aa, ad, da, dd; two rows per step, four sums interleaved */
+    if (lane < FC) {
+        const __amdgpu_buffer_rsrc_t rP =
+            __builtin_amdgcn_make_buffer_rsrc(g.P[item] + (int64_t)b * a.P_bs, 0, (int)(4 * a.P_bs), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rA = a.last ? rP
+            : __builtin_amdgcn_make_buffer_rsrc(g.anext[item] + (int64_t)b * a.Ro * a.Co, 0, 4 * a.Ro * a.Co, 0x00020000);
+        const int pitchA = a.last ? a.PC : a.Co;
+        const int voff = 4 * (o0c + lane);
+        auto flo = [&](int k) { return (k & 1) ? tp.t[k >> 1].y : tp.t[k >> 1].x; };
+        constexpr int NW = FB_THREADS / 64;
+        static_assert(FR % (2 * NW) == 0, "row pairs per wave");
+#pragma unroll
+        for (int pr = 0; pr < FR / (2 * NW); ++pr) {
+            const int oA = wv + 2 * NW * pr, oB = oA + NW;
+            f2 vA[FT], vB[FT];
+#pragma unroll
+            for (int j = 0; j < FT; ++j) { /* sample cc = 2 lane + FT - 1 - j of the row */
+                const float2 xa = LH[lhi(oA, 2 * lane + FT - 1 - j)], xb = LH[lhi(oB, 2 * lane + FT - 1 - j)];
+                vA[j] = f2{xa.x, xa.y};
+                vB[j] = f2{xb.x, xb.y};
+            }
+            const f2 z2 = {0.0f, 0.0f};
+            f2 aA = z2 + flo(0) * vA[0], dA = z2 + flo(1) * vA[0], aB = z2 + flo(0) * vB[0], dB = z2 + flo(1) * vB[0];
+#pragma unroll
+            for (int j = 1; j < FT; ++j) {
+                const float tl = flo(2 * j), th = flo(2 * j + 1);
+                aA = aA + tl * vA[j];
+                dA = dA + th * vA[j];
+                aB = aB + tl * vB[j];
+                dB = dB + th * vB[j];
+            }
+            /* low = (aa, da), high = (ad, dd) */
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int r = o0r + (u ? oB : oA);
+                const f2 lw = u ? aB : aA, hg = u ? dB : dA;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.x), rA, voff, 4 * r * pitchA, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.x), rP, voff, 4 * (r * a.PC + a.offC), 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.y), rP, voff, 4 * ((a.offR + r) * a.PC), 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.y), rP, voff, 4 * ((a.offR + r) * a.PC + a.offC), 0);
+            }
+        }
+    }
+    WTP_FPROBE(3);
+}
+
 /* ------------------------------------------------------------ synthesis --- */
 struct InvArgs {
     const float* a;      /* approximation (B, R, C) with row pitch lda, batch stride a_bs */
@@ -498,6 +672,7 @@ struct InvArgs {
     const float* thr;    /* per-tensor float32 threshold applied to packed coefficients */
     unsigned long long* zc;
     int tilesC, tilesR;
+    int tr0, nTR, tc0, nTC, frame; /* as FwdArgs: k_inv_int's rectangle, k_inv_level's frame */
 };
 
 /* the inverse's items of one geometry: per item its approximation source, packed array and output,
@@ -527,7 +702,16 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
     a.thr = a.thr ? a.thr + g.thr_off[item] : nullptr;
     a.zc = a.zc ? a.zc + g.zc_off[item] : nullptr;
     const int tile = gt - item * g.tiles;
-    const int tc = tile % a.tilesC, tr = (tile / a.tilesC) % a.tilesR, b = tile / (a.tilesC * a.tilesR);
+    int tc, tr, b;
+    if (a.frame) {
+        const int per = a.tilesR * a.tilesC - a.nTR * a.nTC;
+        b = tile / per;
+        frame_tile(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, &tr, &tc);
+    } else {
+        tc = tile % a.tilesC;
+        tr = (tile / a.tilesC) % a.tilesR;
+        b = tile / (a.tilesC * a.tilesR);
+    }
     const int n0 = tr * IR, m0 = tc * IC;
     const int nl = min(n0 + IR, a.outH) - 1, ml = min(m0 + IC, a.outW) - 1;
     const int r_lo = site_u(n0, a.R, F).iu - H + 1, r_hi = site_u(nl, a.R, F).iu;
@@ -789,7 +973,187 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
     WTP_FPROBE(3);
 }
 
+/* One synthesis level over the INTERIOR tiles of a group (InvGroup geo: tr0/nTR/tc0/nTC): every
+ * output of the tile is a full-tile non-special site whose coefficient window lies inside the
+ * level (no wrap), so the tile's coefficient rows / columns are exactly IR/2 + H - (H & 1) and
+ * only wt_syn_pass's ascending interior order occurs; the frame of edge tiles runs k_inv_level.
+ * Same sums in the same order as k_inv_level's interior forms (from 0, as pywt).  Instruction shape: coefficient loads are buffer loads
+ * whose four subband offsets are scalars (one lane offset per element), the row pass's per-lane
+ * taps are register pairs broadcast by op_sel, the output stores take the row as a scalar
+ * offset, and zeros are counted by ballot. */
+template <int FT>
+__global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup g, SmallTaps tp) {
+    static_assert(FT > 0 && FT % 2 == 0, "specialised even filters");
+    extern __shared__ float lds[];
+    constexpr int H = FT / 2, HM = H;
+    constexpr int NR = IR / 2 + H - (H & 1), NC = IC / 2 + H - (H & 1); /* coefficient rows / columns */
+    const int gt = xcd_tile(blockIdx.x, gridDim.x);
+    const int item = gt / g.tiles;
+    const InvArgs& a = g.geo;
+    const int tile = gt - item * g.tiles;
+    const int per = a.nTR * a.nTC;
+    const int b = tile / per, t2 = tile - b * per;
+    const int trr = t2 / a.nTC;
+    const int n0 = (a.tr0 + trr) * IR, m0 = (a.tc0 + t2 - trr * a.nTC) * IC;
+    const int r_lo = site_u(n0, a.R, FT).iu - H + 1, c_lo = site_u(m0, a.C, FT).iu - H + 1;
+    float2* Aq = reinterpret_cast<float2*>(lds); /* (cA, cH=da) */
+    float2* Dq = Aq + NR * NC;                   /* (cV=ad, cD=dd) */
+    float2* LoHi = Aq;                           /* NR x IC, written over Aq/Dq after the row pass */
+    const float* thrp = a.thr ? a.thr + g.thr_off[item] : nullptr;
+    const float thr = thrp ? *thrp : 0.0f; /* |c| < 0 never holds: no threshold */
+    auto tl = [&](float c) { return (fabsf(c) < thr) ? 0.0f : c; };
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    WTP_FPROBE(0);
+    /* 1. the four coefficient tiles, thresholded on load: element e of the NR x NC window at
+     *    lane offset (r_lo + rr) * PC + c_lo + cc; the subbands differ by scalar offsets */
+    {
+        const __amdgpu_buffer_rsrc_t rP =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.P[item]) + (int64_t)b * a.P_bs, 0, (int)(4 * a.P_bs), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rA = a.a_from_P ? rP
+            : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.a[item]) + (int64_t)b * a.a_bs, 0, (int)(4 * a.a_bs), 0x00020000);
+        const int sV = 4 * a.offC, sH = 4 * a.offR * a.PC, sD = sH + sV;
+        constexpr int NE = NR * NC, K = (NE + FB_THREADS - 1) / FB_THREADS;
+        float4 q[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int e = min(k * FB_THREADS + (int)threadIdx.x, NE - 1);
+            const int rr = e / NC, cc = e - rr * NC;
+            const int r = r_lo + rr, c = c_lo + cc;
+            const int vo = 4 * (r * a.PC + c);
+            const int va = a.a_from_P ? vo : 4 * (r * a.lda + c);
+            q[k].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rA, va, 0, 0));
+            q[k].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rP, vo, sV, 0));
+            q[k].z = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rP, vo, sH, 0));
+            q[k].w = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rP, vo, sD, 0));
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) { /* clamped duplicates rewrite their own value */
+            const int e = min(k * FB_THREADS + (int)threadIdx.x, NE - 1);
+            const float va = a.a_from_P ? tl(q[k].x) : q[k].x;
+            Aq[e] = make_float2(va, tl(q[k].z));
+            Dq[e] = make_float2(tl(q[k].y), tl(q[k].w));
+        }
+    }
+    __syncthreads();
+    WTP_FPROBE(1);
+    /* 2. axis -1 synthesis of the NR coefficient rows.  Lane = (row ro = lane / 32 of a row pair,
+     *    column slot c = lane % 32); sub-pass p computes output column m0 + 2c + p, so the output's
+     *    parity -- its taps -- and its site offset are uniform: the taps stay scalar.  A wave takes
+     *    the row pairs wv, wv + 4, ...; results wait in registers until every read of Aq/Dq is done
+     *    (LoHi is written over them). */
+    const int m = m0 + lane;
+    constexpr int KP = (NR + 7) / 8; /* row pairs per wave */
+    f2 rowres[KP][2];
+    {
+        const int ro = lane >> 5, c = lane & 31;
+        /* both sub-passes from one sample window: p's samples start at column c + pe(p), and the
+         * two sums are independent chains that interleave */
+        constexpr int PE1 = (H & 1) ? 0 : 1, NS = HM + PE1;
+        constexpr int PAR0 = (H & 1) ? 0 : 1, PAR1 = 1 - PAR0;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            const int row = min(2 * (wv + 4 * k) + ro, NR - 1);
+            const float2* pa = Aq + row * NC + c;
+            const float2* pd = Dq + row * NC + c;
+            f2 v[NS];
+            /* sample of sub-pass p at tap j: column c + pe(p) + HM - 1 - j */
+            auto sp = [&](int p, int j) { return v[(p ? PE1 : 0) + HM - 1 - j]; };
+#pragma unroll
+            for (int q = 0; q < NS; ++q) { const float2 t = pa[q]; v[q] = f2{t.x, t.y}; }
+            const f2 z2 = {0.0f, 0.0f};
+            f2 a0 = z2 + tp.f[2][PAR0] * sp(0, 0), a1 = z2 + tp.f[2][PAR1] * sp(1, 0);
+#pragma unroll
+            for (int j = 1; j < HM; ++j) {
+                a0 = a0 + tp.f[2][2 * j + PAR0] * sp(0, j);
+                a1 = a1 + tp.f[2][2 * j + PAR1] * sp(1, j);
+            }
+#pragma unroll
+            for (int q = 0; q < NS; ++q) { const float2 t = pd[q]; v[q] = f2{t.x, t.y}; }
+#pragma unroll
+            for (int j = 0; j < HM; ++j) {
+                a0 = a0 + tp.f[3][2 * j + PAR0] * sp(0, j);
+                a1 = a1 + tp.f[3][2 * j + PAR1] * sp(1, j);
+            }
+            /* computed HERE: without this the compiler sinks the sums past the barrier below
+             * (their only use is the LoHi write) and keeps every sample alive across it */
+            asm volatile("" : "+v"(a0), "+v"(a1));
+            rowres[k][0] = a0;
+            rowres[k][1] = a1;
+        }
+    }
+    __syncthreads(); /* every read of Aq/Dq is done: LoHi overwrites them */
+    {
+        const int ro = lane >> 5, c = lane & 31;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            const int row = 2 * (wv + 4 * k) + ro;
+            if (row < NR) {
+#pragma unroll
+                for (int p = 0; p < 2; ++p) LoHi[row * IC + 2 * c + p] = make_float2(rowres[k][p].x, rowres[k][p].y);
+            }
+        }
+    }
+    __syncthreads();
+    WTP_FPROBE(2);
+    /* 3. axis -2: each wave owns RB consecutive output rows; outputs k and k + RB/2 share taps and
+     *    sit four sites apart, computed packed from the block's LoHi rows held in registers */
+    constexpr int RB = IR / (FB_THREADS / 64);
+    constexpr int E = (H & 1) ? 0 : 1, NV = H + RB / 2 - 1 + E, RB2 = RB / 2;
+    static_assert(RB % 4 == 0, "packed column blocks pair rows k and k + RB/2, RB/4 sites apart");
+    const int nf = n0 + RB * wv;
+    const int g0 = site_u(nf, a.R, FT).i - H + 1 - r_lo;
+    float2 r[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) r[q] = LoHi[(g0 + q) * IC + lane];
+    f2 acc[RB2];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        const float t0 = tp.f[2][2 * j], t1 = tp.f[2][2 * j + 1];
+#pragma unroll
+        for (int k = 0; k < RB2; ++k) {
+            const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
+            const float t = par ? t1 : t0;
+            const f2 p = f2{t, t} * f2{r[base - j].x, r[base - j + RB2 / 2].x};
+            acc[k] = (j == 0 ? f2{0.0f, 0.0f} : acc[k]) + p;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        const float t0 = tp.f[3][2 * j], t1 = tp.f[3][2 * j + 1];
+#pragma unroll
+        for (int k = 0; k < RB2; ++k) {
+            const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
+            const float t = par ? t1 : t0;
+            acc[k] = acc[k] + f2{t, t} * f2{r[base - j].y, r[base - j + RB2 / 2].y};
+        }
+    }
+    const __amdgpu_buffer_rsrc_t rY =
+        __builtin_amdgcn_make_buffer_rsrc(g.y[item] + (int64_t)b * a.outH * a.outW, 0, 4 * a.outH * a.outW, 0x00020000);
+    const int vy = 4 * m;
+    uint32_t z = 0; /* wave-uniform: zeros of this wave's outputs */
+#pragma unroll
+    for (int k = 0; k < RB2; ++k) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[k].x), rY, vy, 4 * (nf + k) * a.outW, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[k].y), rY, vy, 4 * (nf + k + RB2) * a.outW, 0);
+        z += (uint32_t)__popcll(__ballot(acc[k].x == 0.0f)) + (uint32_t)__popcll(__ballot(acc[k].y == 0.0f));
+    }
+    if (a.zc) {
+        __shared__ uint32_t zs;
+        if (threadIdx.x == 0) zs = 0;
+        __syncthreads();
+        if (lane == 0 && z) atomicAdd(&zs, z);
+        __syncthreads();
+        if (threadIdx.x == 0 && zs) atomicAdd(a.zc + g.zc_off[item], (unsigned long long)zs);
+    }
+    WTP_FPROBE(3);
+}
+
 /* ------------------------------------------------------------ launchers --- */
+/* interior tiles in their own kernels (k_fwd_int): on by default; 0 runs every tile in
+ * k_fwd_level (A/B and parity cross-checks) */
+static std::atomic<int> g_fb_interior{1};
+int fb_set_interior(int mode) { return g_fb_interior.exchange(mode ? 1 : 0); }
+
 /* dynamic LDS per workgroup; `alias`: the specialised kernels write their second-pass input
  * over their first-pass input (k_fwd_level: LH over T; k_inv_level: LoHi over Aq/Dq) */
 static size_t fwd_lds(int F, bool alias = false) {
@@ -823,8 +1187,70 @@ static void fwd_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
     hipLaunchKernelGGL(k_fwd_level<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, FT > 0), s, g, taps_of<FT>(tp));
 }
 template <int FT>
+static void fwd_int_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
+    FwdIntTaps t;
+    memset(&t, 0, sizeof t);
+    for (int j = 0; j < FT; ++j) t.t[j] = f2{tp.f[0][j], tp.f[1][j]};
+    hipLaunchKernelGGL(k_fwd_int<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, true), s, g, t);
+}
+
+/* The interior rectangle of a forward level's tile grid (k_fwd_int's tiles): a tile row is
+ * interior when its input rows lie inside the image (no extension; then every output site of it
+ * is interior too, i < R) and it is full; a tile column when its aligned float4 window
+ * [gc0 - S0, gc0 - S0 + TP) lies inside the row and it is full.  Both conditions are intervals
+ * of the tile index.  False: no interior tile (or offsets beyond the kernel's 32-bit buffer
+ * offsets) -- k_fwd_level takes the whole grid. */
+static bool fwd_interior(const FwdArgs& a, int F, int* r0, int* nr, int* c0, int* nc) {
+    if (!a.al16 || (int64_t)4 * a.P_bs > INT32_MAX || (int64_t)4 * a.Ro * a.Co > INT32_MAX) return false;
+    const int S0 = ((1 - F / 2) % 4 + 4) % 4, TP = (S0 + 2 * FC + F - 2 + 3) / 4 * 4, NR = 2 * FR + F - 2;
+    int rlo = -1, rhi = -2, clo = -1, chi = -2;
+    for (int tr = 0; tr < a.tilesR; ++tr) {
+        const int gr0 = 2 * FR * tr - F / 2 + 1;
+        if (gr0 >= 0 && gr0 + NR <= a.R && (tr + 1) * FR <= a.Ro) { if (rlo < 0) rlo = tr; rhi = tr; }
+    }
+    for (int tc = 0; tc < a.tilesC; ++tc) {
+        const int st = 2 * FC * tc - F / 2 + 1 - S0;
+        if (st >= 0 && st + TP <= a.C && (tc + 1) * FC <= a.Co) { if (clo < 0) clo = tc; chi = tc; }
+    }
+    if (rlo < 0 || clo < 0) return false;
+    *r0 = rlo; *nr = rhi - rlo + 1; *c0 = clo; *nc = chi - clo + 1;
+    return true;
+}
+static bool fwd_int_filter(int F) { return F == 2 || F == 4 || F == 6 || F == 8 || F == 10 || F == 12 || F == 16 || F == 18; }
+template <int FT>
 static void inv_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
     hipLaunchKernelGGL(k_inv_level<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F, FT > 0), s, g, taps_of<FT>(tp));
+}
+template <int FT>
+static void inv_int_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
+    hipLaunchKernelGGL(k_inv_int<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F, true), s, g, taps_of<FT>(tp));
+}
+
+/* The interior rectangle of a synthesis level's tile grid (k_inv_int's tiles): along each axis a
+ * tile is interior when it is full, holds no special site (H even: outputs 0 and 2N - 1), its
+ * last site is below N and its first site's window starts at or after 0 -- the sites grow with
+ * the output index, so the interior tiles are an interval. */
+static bool inv_axis(int tiles, int T, int out, int N, int F, int* lo, int* cnt) {
+    const int H = F / 2;
+    int a = -1, z = -2;
+    for (int t = 0; t < tiles; ++t) {
+        const int n0 = t * T, nl = n0 + T - 1;
+        if (nl >= out) continue;
+        const wt_syn_site s0 = wt_syn_locate(n0, N, F), s1 = wt_syn_locate(nl, N, F);
+        if (s0.special || s1.special || (H % 2 == 0 && (n0 == 0 || nl >= 2 * N - 1))) continue;
+        if (s1.i >= N || s0.i - H + 1 < 0) continue;
+        if (a < 0) a = t;
+        z = t;
+    }
+    if (a < 0) return false;
+    *lo = a;
+    *cnt = z - a + 1;
+    return true;
+}
+static bool inv_interior(const InvArgs& a, int F, int* r0, int* nr, int* c0, int* nc) {
+    if ((int64_t)4 * a.P_bs > INT32_MAX || (int64_t)4 * a.outH * a.outW > INT32_MAX) return false;
+    if (!a.a_from_P && (int64_t)4 * a.a_bs > INT32_MAX) return false;
+    return inv_axis(a.tilesR, IR, a.outH, a.R, F, r0, nr) && inv_axis(a.tilesC, IC, a.outW, a.C, F, c0, nc);
 }
 
 /* The tiled path needs an even filter, the LDS budget, and images large enough that a tile
@@ -837,6 +1263,7 @@ bool fb_tiled_ok(int64_t B, int64_t R, int64_t C, const Taps& tp) {
 
 static FwdArgs fwd_args(const FwdItem& x) {
     FwdArgs a;
+    memset(&a, 0, sizeof a);
     a.in = x.in;
     a.in_bs = x.R * x.C;
     a.R = (int)x.R;
@@ -858,6 +1285,7 @@ static FwdArgs fwd_args(const FwdItem& x) {
 
 static InvArgs inv_args(const InvItem& x) {
     InvArgs a;
+    memset(&a, 0, sizeof a);
     a.a = x.a_src ? x.a_src : x.P;
     a.a_bs = x.a_bs;
     a.lda = (int)x.lda;
@@ -930,6 +1358,31 @@ void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) 
             g.anext[m] = args[grp[m]].anext;
             g.P[m] = args[grp[m]].P;
         }
+        int r0, nr, c0, nc;
+        if (g_fb_interior.load(std::memory_order_relaxed) && fwd_int_filter(tp.F) &&
+            fwd_interior(g.geo, tp.F, &r0, &nr, &c0, &nc)) {
+            /* the interior tiles in k_fwd_int, the frame around them in k_fwd_level */
+            const int B = g.tiles / (g.geo.tilesR * g.geo.tilesC);
+            g.geo.tr0 = r0; g.geo.nTR = nr; g.geo.tc0 = c0; g.geo.nTC = nc;
+            FwdGroup gi = g;
+            gi.tiles = nr * nc * B;
+            const int gridi = gi.n * gi.tiles;
+            switch (tp.F) {
+            case 2: fwd_int_go<2>(gi, gridi, tp, s); break;
+            case 4: fwd_int_go<4>(gi, gridi, tp, s); break;
+            case 6: fwd_int_go<6>(gi, gridi, tp, s); break;
+            case 8: fwd_int_go<8>(gi, gridi, tp, s); break;
+            case 10: fwd_int_go<10>(gi, gridi, tp, s); break;
+            case 12: fwd_int_go<12>(gi, gridi, tp, s); break;
+            case 16: fwd_int_go<16>(gi, gridi, tp, s); break;
+            case 18: fwd_int_go<18>(gi, gridi, tp, s); break;
+            default: break;
+            }
+            const int fr = g.geo.tilesR * g.geo.tilesC - nr * nc;
+            if (fr == 0) continue;
+            g.geo.frame = 1;
+            g.tiles = fr * B;
+        }
         const int grid = g.n * g.tiles;
         switch (tp.F) {
         case 2: fwd_go<2>(g, grid, tp, s); break;
@@ -979,6 +1432,31 @@ void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s) 
             g.y[m] = x.y;
             g.thr_off[m] = x.thr ? (int32_t)(x.thr - g.geo.thr) : 0;
             g.zc_off[m] = x.zc ? (int32_t)(x.zc - g.geo.zc) : 0;
+        }
+        int r0, nr, c0, nc;
+        if (g_fb_interior.load(std::memory_order_relaxed) && fwd_int_filter(tp.F) &&
+            inv_interior(g.geo, tp.F, &r0, &nr, &c0, &nc)) {
+            /* the interior tiles in k_inv_int, the frame around them in k_inv_level */
+            const int B = g.tiles / (g.geo.tilesR * g.geo.tilesC);
+            g.geo.tr0 = r0; g.geo.nTR = nr; g.geo.tc0 = c0; g.geo.nTC = nc;
+            InvGroup gi = g;
+            gi.tiles = nr * nc * B;
+            const int gridi = gi.n * gi.tiles;
+            switch (tp.F) {
+            case 2: inv_int_go<2>(gi, gridi, tp, s); break;
+            case 4: inv_int_go<4>(gi, gridi, tp, s); break;
+            case 6: inv_int_go<6>(gi, gridi, tp, s); break;
+            case 8: inv_int_go<8>(gi, gridi, tp, s); break;
+            case 10: inv_int_go<10>(gi, gridi, tp, s); break;
+            case 12: inv_int_go<12>(gi, gridi, tp, s); break;
+            case 16: inv_int_go<16>(gi, gridi, tp, s); break;
+            case 18: inv_int_go<18>(gi, gridi, tp, s); break;
+            default: break;
+            }
+            const int fr = g.geo.tilesR * g.geo.tilesC - nr * nc;
+            if (fr == 0) continue;
+            g.geo.frame = 1;
+            g.tiles = fr * B;
         }
         const int grid = g.n * g.tiles;
         switch (tp.F) {

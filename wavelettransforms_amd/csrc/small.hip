@@ -299,23 +299,16 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     __shared__ uint32_t s_bef[2];
     __shared__ float staps[4][SM_F_MAX]; /* dec_lo, dec_hi, rec_lo, rec_hi */
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t q = head->parity;
+    /* the workspace parity by a VECTOR load, made uniform only once the level-0 window's loads have
+     * returned (its wait is then free): a scalar load of it is waited by the first LDS barrier and
+     * put a device round trip ahead of the window's loads */
+    const uint32_t qv = sm_ldc(&head->parity);
     if (t.stamps && tid == 0) atomicMin(t.stamps, sm_ticks()); /* measurement only */
-    {   /* clear this workgroup's slice of the idle region (the previous launch's) */
-        uint4* idle = reinterpret_cast<uint4*>(sel_region(head, q ^ 1u));
-        constexpr int NV4 = (int)(SEL_REGION / 16);
-        const int per = (NV4 + (int)gridDim.x - 1) / (int)gridDim.x;
-        for (int i = tid; i < per; i += SM_THREADS) {
-            const int j = (int)blockIdx.x * per + i;
-            if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
-        }
-    }
     SM_PROBE(6);
     int si = 0;
 #pragma unroll
     for (int i = 1; i < SM_MAX_SEG; ++i) si += (int)blockIdx.x >= t.wg_begin[i];
     const SmallSeg& g = t.s[si];
-    SmallState* st = reinterpret_cast<SmallState*>(sel_region(head, q)) + si;
     const int F = FT ? FT : t.tp.F;
     const int L = g.L;
     const int lt = (int)blockIdx.x - g.wg_begin;
@@ -389,6 +382,18 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                 const int e = e0 + tid + u * SM_THREADS;
                 if (e < n) X[e] = v[u];
             }
+        }
+    }
+    uint32_t q;
+    asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(q) : "v"(qv) : "memory");
+    SmallState* st = reinterpret_cast<SmallState*>(sel_region(head, q)) + si;
+    {   /* clear this workgroup's slice of the idle region (the previous launch's) */
+        uint4* idle = reinterpret_cast<uint4*>(sel_region(head, q ^ 1u));
+        constexpr int NV4 = (int)(SEL_REGION / 16);
+        const int per = (NV4 + (int)gridDim.x - 1) / (int)gridDim.x;
+        for (int i = tid; i < per; i += SM_THREADS) {
+            const int j = (int)blockIdx.x * per + i;
+            if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
         }
     }
     __syncthreads();
@@ -529,7 +534,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
         const uint32_t nsh = (gridDim.x - sh + NSHARD - 1) / NSHARD; /* workgroups of this shard */
         const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);     /* shards with workgroups */
         if (atomicAdd(&br->arrive[sh][0], 1u) == nsh - 1u && atomicAdd(&br->arrive[0][16], 1u) == nact - 1u)
-            sm_stc(&head->parity, q ^ 1u);
+            sm_stc(&head->parity, q + 1u);
     }
     bool ok = sm_wait(&st->bar[0][0], a0, nwg, tmo, &s_ok);
     SM_PROBE(11);

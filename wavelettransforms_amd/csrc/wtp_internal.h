@@ -91,6 +91,7 @@ struct SegDesc {
     int64_t cap;       /* nsub * bucket_cap                                              */
     int32_t nsub_log2; /* 6..10                                                          */
     int32_t bucket_cap;
+    uint64_t res_step_fx; /* k_resident: (n - SAMPLE_GROUP) / (RES_MS / SAMPLE_GROUP - 1) in 32.32 fixed point */
 };
 
 struct SegTable {
@@ -146,8 +147,10 @@ struct alignas(128) BarState {
     uint32_t arrive[NSHARD][32];
 };
 constexpr size_t SEL_REGION = SEG_PER_LAUNCH * sizeof(SelState) + sizeof(BarState);
+/* the parity word counts selection launches (every launch's last arrival adds 1); its low bit
+ * picks the region */
 __host__ __device__ inline SelState* sel_region(void* head, uint32_t q) {
-    return reinterpret_cast<SelState*>(reinterpret_cast<char*>(head) + sizeof(SelHeader) + (size_t)q * SEL_REGION);
+    return reinterpret_cast<SelState*>(reinterpret_cast<char*>(head) + sizeof(SelHeader) + (size_t)(q & 1u) * SEL_REGION);
 }
 __host__ __device__ inline BarState* bar_region(void* head, uint32_t q) {
     return reinterpret_cast<BarState*>(reinterpret_cast<char*>(sel_region(head, q)) + SEG_PER_LAUNCH * sizeof(SelState));
@@ -193,10 +196,15 @@ constexpr int RES_LATE_PCT = 45;
 constexpr int RES_STG = 32;                         /* inside keys a thread may stage (of its 96; ~11 expected) */
 /* After the first segment barrier every workgroup publishes the keys of the (one or two)
  * buckets holding the segment's ranks in a slot of its own: word 0 the count, then the keys */
-/* one workgroup's published region in the candidate area: its bucket offsets (RES_NSUB + 1 words,
- * padded to 16 bytes), then its inside keys bucket-sorted (at most RES_STG per thread) */
-constexpr int RES_PUB_KEYS = (RES_NSUB + 1 + 3) / 4 * 4;
-constexpr int RES_PUB_WORDS = RES_PUB_KEYS + RES_STG * RES_THREADS;
+/* one workgroup's published region in the candidate area: one slot of RES_SLOT words per bucket,
+ * [tag, count, keys...] -- the tag (RES_SLOT_TAG | the launch's parity counter) tells this launch's
+ * slots from older ones (an empty bucket writes nothing and keeps an older tag); keys and every
+ * other layout that shares the area have bits 31..30 clear.  A reader takes the first RES_SLOT0
+ * words of a slot in one round trip (RES_SLOT0 - 2 keys), the rest only for a fuller bucket. */
+constexpr int RES_SLOT = 32;
+constexpr int RES_SLOT0 = 16;
+constexpr uint32_t RES_SLOT_TAG = 0xC0000000u;
+constexpr int RES_PUB_WORDS = RES_NSUB * RES_SLOT;
 constexpr int RES_WG_WORDS = RES_PUB_WORDS;
 constexpr int RES_SEL_MAX = 1024;                   /* keys the one-wave select takes (more: full scan) */
 constexpr uint32_t RES_TIMEOUT_DEFAULT_US = 200000; /* a wait this long means the grid is not co-resident */
@@ -297,6 +305,7 @@ struct InvItem { /* one image batch's synthesis level k -> y (B, outH, outW) */
 };
 void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s);
 void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s);
+int fb_set_interior(int mode); /* interior filter-bank kernels on (1, default) / off; returns the previous */
 void launch_fwd_level(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* anext, float* P,
                       int64_t PR, int64_t PC, int64_t offR, int64_t offC, int last, hipStream_t s);
 void launch_inv_level(const float* a_src, int64_t a_bs, int64_t lda, int a_from_P, const float* P, int64_t PR,

@@ -227,6 +227,12 @@ def set_pipeline(enabled):
     return bool(N.lib().wtp_set_pipeline(1 if enabled else 0))
 
 
+def set_interior(enabled):
+    """Run the filter-bank levels' interior tiles in their edge-free kernels (default) or every
+    tile in the general kernel (include/wtprune.h wtp_set_interior); returns the previous setting."""
+    return bool(N.lib().wtp_set_interior(1 if enabled else 0))
+
+
 def resident_capacity():
     """Workgroups (of 49152 weights) the resident launch can hold on the current device; 0: never used."""
     return int(N.lib().wtp_resident_capacity())
