@@ -45,7 +45,7 @@ VALU_NOFMA_TFLOPS = 128.0
 METRIC = "weight-coeffs/s for L5 bior3.3 DWT+thresh+IDWT; achieved HBM GB/s vs peak"
 STAGES = ["forward_dwt", "k_window", "k_collect", "k_mask_select", "inverse_dwt"]
 KERNEL_OF_STAGE = {"k_window": "k_window", "k_collect": "k_collect_t", "k_mask_select": "k_mask_select",
-                   "forward_dwt": "k_fwd_level", "inverse_dwt": "k_inv_level"}
+                   "forward_dwt": "k_fwd_int+k_fwd_level", "inverse_dwt": "k_inv_int+k_inv_level"}
 DWT_STAGES = ("forward_dwt", "inverse_dwt")
 CFG5_BLOCKS = 64
 DB8_L5_FLOP_PER_ELEM = 170.5  # 4 F sum_k 4^-k MACs, no FMA, F = 16, L = 5
@@ -155,9 +155,10 @@ def rocprof_kernel(stats, kernel):
     """(total ns, launches) of the wtp kernel named `kernel` (every template instance) in a
     rocprof_child summary; (0.0, 0) if absent."""
     calls, total = 0, 0.0
+    want = {"wtp::" + k for k in kernel.split("+")}  # a stage's kernels ("a+b": interior + frame)
     for name, (c, t) in (stats or {}).items():
         base = name.split("(")[0].split("<")[0].replace("void ", "").strip()
-        if base == "wtp::" + kernel:
+        if base in want:
             calls += c
             total += t
     return total, calls

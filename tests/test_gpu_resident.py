@@ -305,3 +305,28 @@ def test_solo_overflow_then_reuse(eng, n):
             ref, rr = O.prune_tensor(x.copy(), "haar", 0, 50.0)
             _same(outs[0].cpu().numpy(), ref, r, rr)
             assert r["path"] != eng.MODE_FAULT
+
+
+@pytest.mark.parametrize("ties", [3, 20, 60])
+def test_slot_overflow_paths(eng, mode, ties):
+    """k_resident's published bucket slots hold 14 keys in the granules every reader fetches, 30 in
+    all: `ties` copies of the segment's median value inside ONE workgroup's chunk put that many
+    keys into one slot of the ranks' bucket -- 3 fit the first granules, 20 take the second round
+    trip, 60 overflow the slot (full scan).  Exact either way, and the next call on the workspace
+    too."""
+    n = 4 * RES_CHUNK
+    rng = np.random.default_rng(ties)
+    x = (rng.standard_normal(n) * 0.05).astype(np.float32)
+    pos = RES_CHUNK + 100 + np.arange(ties)
+    rest = np.delete(np.abs(x), pos)
+    v = np.float32(np.sort(rest)[len(rest) // 2])
+    x[pos] = v * np.where(rng.random(ties) < 0.5, -1, 1).astype(np.float32)
+    for pct in (50.0, 49.99):
+        outs, (r,) = eng.prune([_dev(x)], "haar", 0, pct)
+        ref, rr = O.prune_tensor(x.copy(), "haar", 0, pct)
+        _same(outs[0].cpu().numpy(), ref, r, rr)
+        assert r["path"] != eng.MODE_FAULT
+    y = (rng.standard_normal(n) * 0.05).astype(np.float32)
+    outs, (r,) = eng.prune([_dev(y)], "haar", 0, 50.0)
+    ref, rr = O.prune_tensor(y.copy(), "haar", 0, 50.0)
+    _same(outs[0].cpu().numpy(), ref, r, rr)

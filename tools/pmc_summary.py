@@ -17,7 +17,8 @@ import re
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_resident", "k_small", "k_mask_select", "k_mask_inplace", "k_collect_t", "k_window", "k_fwd_level", "k_inv_level", "k_dwt_cols", "k_dwt_rows",
+KERNELS = ["k_resident", "k_small", "k_mask_select", "k_mask_inplace", "k_collect_t", "k_window", "k_fwd_level", "k_inv_level",
+           "k_fwd_int", "k_inv_int", "k_dwt_cols", "k_dwt_rows",
            "k_idwt_rows", "k_idwt_cols", "k_copy_threshold"]
 
 
@@ -58,11 +59,20 @@ def main():
             d["hbm_bytes_per_launch"] = d["fetch_bytes_per_launch"] + d["write_bytes_per_launch"]
         d["launches"] = max(len(v) for v in ctrs.values())
         out["kernels"][k] = d
+    # a filter-bank stage runs as an interior kernel plus a frame kernel per level: their sums
+    # per stage launch pair (bench.py names the stage "k_fwd_int+k_fwd_level")
+    for a, b in (("k_fwd_int", "k_fwd_level"), ("k_inv_int", "k_inv_level")):
+        ka, kb = out["kernels"].get(a), out["kernels"].get(b)
+        if ka and kb and "hbm_bytes_per_launch" in ka and "hbm_bytes_per_launch" in kb:
+            tot = ka["hbm_bytes_per_launch"] * ka["launches"] + kb["hbm_bytes_per_launch"] * kb["launches"]
+            out["kernels"][a + "+" + b] = {"hbm_bytes_per_launch": tot / max(ka["launches"], kb["launches"]),
+                                           "launches": max(ka["launches"], kb["launches"]),
+                                           "note": "interior + frame launches of one level, summed"}
     os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     for k, d in sorted(out["kernels"].items()):
-        print("%-16s fetch %10.0f B  write %10.0f B  launches %d" % (k, d.get("fetch_bytes_per_launch", -1),
+        print("%-24s fetch %10.0f B  write %10.0f B  launches %d" % (k, d.get("fetch_bytes_per_launch", -1),
                                                                    d.get("write_bytes_per_launch", -1), d["launches"]))
 
 

@@ -225,6 +225,7 @@ void launch_resident(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_res
 constexpr int SM_MAX_SEG = 4;       /* tensors per call */
 constexpr int SM_SEG_WG_MAX = 128;  /* workgroups per tensor */
 constexpr int SM_SLOT_WORDS = 64;   /* per workgroup in the candidate region: the keys of the rank's bin */
+constexpr int SM_PUB_BINS_HOST = 32; /* = small.hip's SM_PUB_BINS: published bin slots per workgroup */
 constexpr int SM_ARENA = 34 * 1024; /* LDS words of a workgroup's arena (136 KB) */
 constexpr int SM_F_MAX = 20;        /* longest filter */
 constexpr int SM_LMAX = 10;         /* = SM_MAX_L of small_geom.h */
