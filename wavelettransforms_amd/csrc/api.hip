@@ -222,9 +222,8 @@ Layout make_layout(std::vector<TPlan>& ps) {
     for (auto& p : ps)
         if (!p.dwt) rwg += (p.pop + RES_CHUNK - 1) / RES_CHUNK;
     ce = std::max(ce, (size_t)std::min<int64_t>(rwg, RES_MAX_WG) * RES_WG_WORDS);
-    /* the one-launch small path keeps one slot of SM_SLOT_WORDS per workgroup there, then each
-     * workgroup's published bins (SM_PUB_BINS slots, small.hip) */
-    ce = std::max(ce, (size_t)RES_MAX_WG * SM_SLOT_WORDS * (1 + SM_PUB_BINS_HOST));
+    /* the one-launch small path keeps one slot of SM_SLOT_WORDS per workgroup there */
+    ce = std::max(ce, (size_t)RES_MAX_WG * SM_SLOT_WORDS);
     off = align_up(off + ce * sizeof(uint32_t));
     L.P = off;
     for (auto& p : ps) {

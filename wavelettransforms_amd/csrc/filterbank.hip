@@ -316,7 +316,7 @@ struct FwdIntTaps {
 
 template <int FT>
 __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGroup g, TapsT<FT> tp) {
-    extern __shared__ float lds[];
+    extern __shared__ __attribute__((aligned(16))) float lds[];
     const int F = FT ? FT : tp.F;
     const int NR = 2 * FR + F - 2, NC = 2 * FC + F - 2;
     float* T = lds;                /* NR x NC input tile */
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
 template <int FT>
 __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup g, FwdIntTaps tp) {
     static_assert(FT > 0 && FT % 2 == 0, "specialised even filters");
-    extern __shared__ float lds[];
+    extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int NRc = 2 * FR + FT - 2, NCc = 2 * FC + FT - 2;
     constexpr int S0 = FWD_S0<FT>, TP = FWD_TP<FT>, W4 = TP / 4;
     constexpr int HALF = (NCc + 1) / 2;
@@ -690,7 +690,7 @@ struct InvGroup {
 
 template <int FT>
 __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGroup g, TapsT<FT> tp) {
-    extern __shared__ float lds[];
+    extern __shared__ __attribute__((aligned(16))) float lds[];
     const int gt = xcd_tile(blockIdx.x, gridDim.x);
     const int F = FT ? FT : tp.F;
     const int H = F / 2;
@@ -984,7 +984,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
 template <int FT>
 __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup g, SmallTaps tp) {
     static_assert(FT > 0 && FT % 2 == 0, "specialised even filters");
-    extern __shared__ float lds[];
+    extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int H = FT / 2, HM = H;
     constexpr int NR = IR / 2 + H - (H & 1), NC = IC / 2 + H - (H & 1); /* coefficient rows / columns */
     const int gt = xcd_tile(blockIdx.x, gridDim.x);
@@ -1138,12 +1138,15 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
         z += (uint32_t)__popcll(__ballot(acc[k].x == 0.0f)) + (uint32_t)__popcll(__ballot(acc[k].y == 0.0f));
     }
     if (a.zc) {
-        __shared__ uint32_t zs;
+        /* 8 bytes: the dynamic LDS follows the static variables, and a 4-byte one would leave
+         * every float2 of the tiles 4-byte misaligned (measured: k_inv_int 4x slower, LDS
+         * instruction issue stalls) */
+        __shared__ unsigned long long zs;
         if (threadIdx.x == 0) zs = 0;
         __syncthreads();
-        if (lane == 0 && z) atomicAdd(&zs, z);
+        if (lane == 0 && z) atomicAdd(&zs, (unsigned long long)z);
         __syncthreads();
-        if (threadIdx.x == 0 && zs) atomicAdd(a.zc + g.zc_off[item], (unsigned long long)zs);
+        if (threadIdx.x == 0 && zs) atomicAdd(a.zc + g.zc_off[item], zs);
     }
     WTP_FPROBE(3);
 }
@@ -1153,6 +1156,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
  * k_fwd_level (A/B and parity cross-checks) */
 static std::atomic<int> g_fb_interior{1};
 int fb_set_interior(int mode) { return g_fb_interior.exchange(mode ? 1 : 0); }
+
 
 /* dynamic LDS per workgroup; `alias`: the specialised kernels write their second-pass input
  * over their first-pass input (k_fwd_level: LH over T; k_inv_level: LoHi over Aq/Dq) */
@@ -1336,6 +1340,60 @@ static std::vector<std::vector<int>> uniform_groups(const std::vector<Arg>& args
     return groups;
 }
 
+/* one launch of the general (edge-capable) kernel, and one of the interior kernel, by filter */
+static void fwd_general(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
+    switch (tp.F) {
+    case 2: fwd_go<2>(g, grid, tp, s); break;
+    case 4: fwd_go<4>(g, grid, tp, s); break;
+    case 6: fwd_go<6>(g, grid, tp, s); break;
+    case 8: fwd_go<8>(g, grid, tp, s); break;
+    case 10: fwd_go<10>(g, grid, tp, s); break;
+    case 12: fwd_go<12>(g, grid, tp, s); break;
+    case 16: fwd_go<16>(g, grid, tp, s); break;
+    case 18: fwd_go<18>(g, grid, tp, s); break;
+    default: fwd_go<0>(g, grid, tp, s); break;
+    }
+}
+static void fwd_interior_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
+    switch (tp.F) {
+    case 2: fwd_int_go<2>(g, grid, tp, s); break;
+    case 4: fwd_int_go<4>(g, grid, tp, s); break;
+    case 6: fwd_int_go<6>(g, grid, tp, s); break;
+    case 8: fwd_int_go<8>(g, grid, tp, s); break;
+    case 10: fwd_int_go<10>(g, grid, tp, s); break;
+    case 12: fwd_int_go<12>(g, grid, tp, s); break;
+    case 16: fwd_int_go<16>(g, grid, tp, s); break;
+    case 18: fwd_int_go<18>(g, grid, tp, s); break;
+    default: break;
+    }
+}
+static void inv_general(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
+    switch (tp.F) {
+    case 2: inv_go<2>(g, grid, tp, s); break;
+    case 4: inv_go<4>(g, grid, tp, s); break;
+    case 6: inv_go<6>(g, grid, tp, s); break;
+    case 8: inv_go<8>(g, grid, tp, s); break;
+    case 10: inv_go<10>(g, grid, tp, s); break;
+    case 12: inv_go<12>(g, grid, tp, s); break;
+    case 16: inv_go<16>(g, grid, tp, s); break;
+    case 18: inv_go<18>(g, grid, tp, s); break;
+    default: inv_go<0>(g, grid, tp, s); break;
+    }
+}
+static void inv_interior_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
+    switch (tp.F) {
+    case 2: inv_int_go<2>(g, grid, tp, s); break;
+    case 4: inv_int_go<4>(g, grid, tp, s); break;
+    case 6: inv_int_go<6>(g, grid, tp, s); break;
+    case 8: inv_int_go<8>(g, grid, tp, s); break;
+    case 10: inv_int_go<10>(g, grid, tp, s); break;
+    case 12: inv_int_go<12>(g, grid, tp, s); break;
+    case 16: inv_int_go<16>(g, grid, tp, s); break;
+    case 18: inv_int_go<18>(g, grid, tp, s); break;
+    default: break;
+    }
+}
+
 void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) {
     std::vector<FwdArgs> args(n);
     std::vector<int64_t> tiles(n);
@@ -1361,40 +1419,20 @@ void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) 
         int r0, nr, c0, nc;
         if (g_fb_interior.load(std::memory_order_relaxed) && fwd_int_filter(tp.F) &&
             fwd_interior(g.geo, tp.F, &r0, &nr, &c0, &nc)) {
-            /* the interior tiles in k_fwd_int, the frame around them in k_fwd_level */
+            /* the interior tiles in k_fwd_int, then the frame around them in k_fwd_level (measured
+             * in round 4: the frame on a stream of its own beside the interior launch gained
+             * nothing -- both launches fill every CU, so the work only moved) */
             const int B = g.tiles / (g.geo.tilesR * g.geo.tilesC);
             g.geo.tr0 = r0; g.geo.nTR = nr; g.geo.tc0 = c0; g.geo.nTC = nc;
             FwdGroup gi = g;
             gi.tiles = nr * nc * B;
-            const int gridi = gi.n * gi.tiles;
-            switch (tp.F) {
-            case 2: fwd_int_go<2>(gi, gridi, tp, s); break;
-            case 4: fwd_int_go<4>(gi, gridi, tp, s); break;
-            case 6: fwd_int_go<6>(gi, gridi, tp, s); break;
-            case 8: fwd_int_go<8>(gi, gridi, tp, s); break;
-            case 10: fwd_int_go<10>(gi, gridi, tp, s); break;
-            case 12: fwd_int_go<12>(gi, gridi, tp, s); break;
-            case 16: fwd_int_go<16>(gi, gridi, tp, s); break;
-            case 18: fwd_int_go<18>(gi, gridi, tp, s); break;
-            default: break;
-            }
             const int fr = g.geo.tilesR * g.geo.tilesC - nr * nc;
+            fwd_interior_go(gi, gi.n * gi.tiles, tp, s);
             if (fr == 0) continue;
             g.geo.frame = 1;
             g.tiles = fr * B;
         }
-        const int grid = g.n * g.tiles;
-        switch (tp.F) {
-        case 2: fwd_go<2>(g, grid, tp, s); break;
-        case 4: fwd_go<4>(g, grid, tp, s); break;
-        case 6: fwd_go<6>(g, grid, tp, s); break;
-        case 8: fwd_go<8>(g, grid, tp, s); break;
-        case 10: fwd_go<10>(g, grid, tp, s); break;
-        case 12: fwd_go<12>(g, grid, tp, s); break;
-        case 16: fwd_go<16>(g, grid, tp, s); break;
-        case 18: fwd_go<18>(g, grid, tp, s); break;
-        default: fwd_go<0>(g, grid, tp, s); break;
-        }
+        fwd_general(g, g.n * g.tiles, tp, s);
     }
 }
 
@@ -1436,40 +1474,20 @@ void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s) 
         int r0, nr, c0, nc;
         if (g_fb_interior.load(std::memory_order_relaxed) && fwd_int_filter(tp.F) &&
             inv_interior(g.geo, tp.F, &r0, &nr, &c0, &nc)) {
-            /* the interior tiles in k_inv_int, the frame around them in k_inv_level */
+            /* the interior tiles in k_inv_int, then the frame around them in k_inv_level (measured
+             * in round 4: the frame on a stream of its own beside the interior launch gained
+             * nothing -- both launches fill every CU, so the work only moved) */
             const int B = g.tiles / (g.geo.tilesR * g.geo.tilesC);
             g.geo.tr0 = r0; g.geo.nTR = nr; g.geo.tc0 = c0; g.geo.nTC = nc;
             InvGroup gi = g;
             gi.tiles = nr * nc * B;
-            const int gridi = gi.n * gi.tiles;
-            switch (tp.F) {
-            case 2: inv_int_go<2>(gi, gridi, tp, s); break;
-            case 4: inv_int_go<4>(gi, gridi, tp, s); break;
-            case 6: inv_int_go<6>(gi, gridi, tp, s); break;
-            case 8: inv_int_go<8>(gi, gridi, tp, s); break;
-            case 10: inv_int_go<10>(gi, gridi, tp, s); break;
-            case 12: inv_int_go<12>(gi, gridi, tp, s); break;
-            case 16: inv_int_go<16>(gi, gridi, tp, s); break;
-            case 18: inv_int_go<18>(gi, gridi, tp, s); break;
-            default: break;
-            }
             const int fr = g.geo.tilesR * g.geo.tilesC - nr * nc;
+            inv_interior_go(gi, gi.n * gi.tiles, tp, s);
             if (fr == 0) continue;
             g.geo.frame = 1;
             g.tiles = fr * B;
         }
-        const int grid = g.n * g.tiles;
-        switch (tp.F) {
-        case 2: inv_go<2>(g, grid, tp, s); break;
-        case 4: inv_go<4>(g, grid, tp, s); break;
-        case 6: inv_go<6>(g, grid, tp, s); break;
-        case 8: inv_go<8>(g, grid, tp, s); break;
-        case 10: inv_go<10>(g, grid, tp, s); break;
-        case 12: inv_go<12>(g, grid, tp, s); break;
-        case 16: inv_go<16>(g, grid, tp, s); break;
-        case 18: inv_go<18>(g, grid, tp, s); break;
-        default: inv_go<0>(g, grid, tp, s); break;
-        }
+        inv_general(g, g.n * g.tiles, tp, s);
     }
 }
 

@@ -1332,6 +1332,16 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         if (FULL) load_chunk<IT, CT>(sd.data + base, v);
         else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
         q = parity_late(qv);
+        {   /* clear this workgroup's slice of the idle region (the previous launch's; the next
+             * launch works in it): stores behind the chunk's loads */
+            uint4* idle = reinterpret_cast<uint4*>(sel_region(head, q ^ 1u));
+            constexpr int NV4 = (int)(SEL_REGION / 16);
+            const int per = (NV4 + (int)gridDim.x - 1) / (int)gridDim.x;
+            for (int i = tid; i < per; i += CT) {
+                const int j = (int)blockIdx.x * per + i;
+                if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
+            }
+        }
         /* the parity flip's first-level arrival (the last reader of the parity in the grid flips
          * it): a returning add issued behind wave 7's chunk loads, its result used only at the
          * publication, so its queueing on the shard's counter costs no wave a wait */
@@ -1438,11 +1448,11 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     if (!solo) res_arrive(b1);
     WTP_RPROBE(4);
     /* ---- publication, while the segment gathers at barrier 1: this workgroup's inside keys,
-     * bucket-sorted in LDS, one fixed slot per bucket (tag, count, keys; write-through 16-byte
-     * sc1 stores) in its region of the candidate area, then barrier 2's arrival.  It depends on
-     * nothing global: waves 0-6 store and drain it while wave 7 polls barrier 1, and after the
-     * bucket totals name the ranks' buckets, ONE round trip reads those buckets' slots of every
-     * workgroup of the segment (a fixed place: no offsets to look up first). */
+     * bucket-sorted in LDS, and the bucket offsets (exclusive prefix of its bucket histogram),
+     * write-through (16-byte sc1 stores) to its region of the candidate area, then barrier 2's
+     * arrival.  It depends on nothing global: waves 0-6 store and drain it while wave 7 polls
+     * barrier 1, and after barrier 1 the select reads only the keys of the ranks' buckets from
+     * the regions (offsets, then keys: two round trips) -- no slot round after the locate. */
     uint32_t* pub = cand + (int64_t)blockIdx.x * RES_PUB_WORDS;
     uint32_t* pos = raw;     /* bucket offsets (the window histogram is done with) */
     uint32_t* srt = wstage;  /* the sorted keys, over the columns */
@@ -1522,24 +1532,17 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     } else {
         constexpr int ST = CT - 64; /* the storing threads */
         if (!ovf) {
-            /* bucket b's keys (srt[pos[b - 1] .. pos[b])) into its slot, [tag, count, keys]: only
-             * the 16-byte granules the bucket fills (a count beyond the slot is published as is:
-             * the reader falls back) */
+            /* offsets: pub[b] = start of bucket b (pos[b - 1] now), pub[RES_NSUB] = the total */
             const __amdgpu_buffer_rsrc_t prs = region_rsrc(pub, RES_PUB_WORDS);
-            const uint32_t tag = RES_SLOT_TAG | (q & ~RES_SLOT_TAG);
-            for (int b = tid; b < RES_NSUB; b += ST) {
-                const uint32_t s0 = b ? pos[b - 1] : 0u, c = pos[b] - s0;
-                const int ng = (int)min((c + 5u) / 4u, (uint32_t)(RES_SLOT / 4));
-                for (int gi = 0; gi < (c ? ng : 0); ++gi) {
-                    uint32_t w[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int i = 4 * gi + u - 2; /* key index in the bucket; -2, -1: the header */
-                        w[u] = i == -2 ? tag : (i == -1 ? c : srt[s0 + min((uint32_t)i, c - 1u)]);
-                    }
-                    st16_sc1(prs, b * RES_SLOT + 4 * gi, make_uint4(w[0], w[1], w[2], w[3]));
-                }
+            if (tid < RES_NSUB / 4) {
+                const int b = 4 * tid;
+                st16_sc1(prs, b, make_uint4(b ? pos[b - 1] : 0u, pos[b], pos[b + 1], pos[b + 2]));
+            } else if (tid == RES_NSUB / 4) {
+                stc(pub + RES_NSUB, pos[RES_NSUB - 1]);
             }
+            const uint32_t nin = pos[RES_NSUB - 1];
+            for (uint32_t i4 = tid; 4 * i4 < nin; i4 += ST)
+                st16_sc1(prs, RES_PUB_KEYS + 4 * i4, *reinterpret_cast<const uint4*>(srt + 4 * i4));
         }
         /* every storing wave drains; the last one to do so arrives at barrier 2 for the
          * workgroup (its LDS add follows every other storing wave's drain) */
@@ -1673,77 +1676,53 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 return;
             }
             WTP_PROBE(4);
-            /* ---- the slots of buckets ba and bb (bb != ba) of every workgroup of the segment:
-             * their first RES_SLOT0 words in ONE round trip (every load of a thread in flight
-             * before any is used), staged in LDS over the sorted keys (done with) */
+            /* ---- the segment's workgroups' offsets of buckets ba and bb + 1 (wave 0, every load
+             * in flight at once), their key counts scanned; then the keys themselves, at most two
+             * a thread (m <= RES_SEL_MAX), staged in LDS.  The buckets between ba and bb are
+             * empty, so a workgroup's keys of ba..bb are one run of its sorted array. */
             const int wb = sd.blk_begin;
-            const int nb = bb != ba ? 2 : 1, nsl = (int)nwg * nb;
-            uint32_t* G = wstage; /* RES_SLOT words per slot */
-            const uint32_t tag = RES_SLOT_TAG | (q & ~RES_SLOT_TAG);
-            const __amdgpu_buffer_rsrc_t srs = region_rsrc(cand + (int64_t)wb * RES_PUB_WORDS, (int)nwg * RES_PUB_WORDS);
-            auto slot_word = [&](int sl) { return (sl / nb) * RES_PUB_WORDS + ((sl % nb) ? bb : ba) * RES_SLOT; };
-            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-            {
-                constexpr int G0 = RES_SLOT0 / 4, GPT = (RES_MAX_WG * 2 * G0 + CT - 1) / CT;
-                u4v gv[GPT];
+            __shared__ uint32_t s_so[RES_MAX_WG], s_ob[RES_MAX_WG];
+            __shared__ uint32_t s_tot;
+            if (wv == 0) {
+                constexpr int WPL = RES_MAX_WG / 64;
+                uint32_t ob[WPL], oe[WPL];
 #pragma unroll
-                for (int u = 0; u < GPT; ++u) {
-                    const int i = min(tid + u * CT, nsl * G0 - 1);
-                    gv[u] = __builtin_amdgcn_raw_buffer_load_b128(srs, 4 * (slot_word(i / G0) + 4 * (i % G0)), 0, 16);
+                for (int u = 0; u < WPL; ++u) {
+                    const int w = lane + 64 * u;
+                    const uint32_t* pw = cand + (int64_t)(wb + min(w, (int)nwg - 1)) * RES_PUB_WORDS;
+                    ob[u] = ldc<true>(pw + ba);
+                    oe[u] = ldc<true>(pw + bb + 1);
                 }
+                uint32_t base = 0;
 #pragma unroll
-                for (int u = 0; u < GPT; ++u) {
-                    const int i = min(tid + u * CT, nsl * G0 - 1); /* duplicates rewrite their own value */
-                    *reinterpret_cast<u4v*>(G + (i / G0) * RES_SLOT + 4 * (i % G0)) = gv[u];
+                for (int u = 0; u < WPL; ++u) {
+                    const int w = lane + 64 * u;
+                    const uint32_t cw = w < (int)nwg ? oe[u] - ob[u] : 0u;
+                    const uint32_t inc = wave_scan_u32(cw);
+                    if (w < (int)nwg) { s_so[w] = base + inc - cw; s_ob[w] = ob[u]; }
+                    base += __builtin_amdgcn_readlane(inc, 63);
                 }
+                if (lane == 0) s_tot = base;
             }
             __syncthreads();
-            /* per slot: its count (0 under an older tag); a count past RES_SLOT0 - 2 reads the
-             * rest of its slot (one more round trip, rare), past RES_SLOT - 2 takes the full scan */
-            __shared__ uint32_t s_so[2 * RES_MAX_WG];
-            __shared__ uint32_t s_tot, s_big;
-            if (tid == 0) s_big = 0;
-            __syncthreads();
-            uint32_t cnt_s = 0;
-            if (tid < nsl) {
-                cnt_s = G[tid * RES_SLOT] == tag ? G[tid * RES_SLOT + 1] : 0u;
-                if (cnt_s > (uint32_t)(RES_SLOT0 - 2)) atomicMax(&s_big, cnt_s);
-            }
-            {   /* exclusive scan of the counts over the slots (<= 2 RES_MAX_WG = CT slots) */
-                static_assert(2 * RES_MAX_WG <= CT, "one slot per thread");
-                const uint32_t inc = wave_scan_u32(cnt_s);
-                if (lane == 63) s_wtot[wv] = inc;
-                __syncthreads();
-                uint32_t ex = inc - cnt_s, tot = 0;
-#pragma unroll
-                for (int w = 0; w < NW; ++w) { ex += w < wv ? s_wtot[w] : 0u; tot += s_wtot[w]; }
-                if (tid < nsl) s_so[tid] = ex;
-                if (tid == 0) s_tot = tot;
-            }
-            __syncthreads();
-            if (s_big > (uint32_t)(RES_SLOT - 2) || (int)s_tot != m) {
-                full = true; /* uniform over the segment (the same slots everywhere) */
+            if ((int)s_tot != m) {
+                full = true; /* uniform over the segment (the same regions everywhere) */
             } else {
-                if (s_big) { /* some slot holds more than its first granules: the rest of those */
-                    constexpr int G1 = (RES_SLOT - RES_SLOT0) / 4, GPT1 = (RES_MAX_WG * 2 * G1 + CT - 1) / CT;
-                    u4v gv[GPT1];
+                uint32_t kv[2];
 #pragma unroll
-                    for (int u = 0; u < GPT1; ++u) {
-                        const int i = min(tid + u * CT, nsl * G1 - 1);
-                        gv[u] = __builtin_amdgcn_raw_buffer_load_b128(srs, 4 * (slot_word(i / G1) + RES_SLOT0 + 4 * (i % G1)), 0, 16);
+                for (int u = 0; u < 2; ++u) {
+                    const int i = min(tid + u * CT, m - 1);
+                    int lo_w = 0, hi_w = (int)nwg - 1; /* the last workgroup whose run starts <= i */
+                    while (lo_w < hi_w) {
+                        const int mid = (lo_w + hi_w + 1) >> 1;
+                        if (s_so[mid] <= (uint32_t)i) lo_w = mid; else hi_w = mid - 1;
                     }
+                    kv[u] = ldc<true>(cand + (int64_t)(wb + lo_w) * RES_PUB_WORDS + RES_PUB_KEYS + s_ob[lo_w] +
+                                      ((uint32_t)i - s_so[lo_w]));
+                }
 #pragma unroll
-                    for (int u = 0; u < GPT1; ++u) {
-                        const int i = min(tid + u * CT, nsl * G1 - 1);
-                        *reinterpret_cast<u4v*>(G + (i / G1) * RES_SLOT + RES_SLOT0 + 4 * (i % G1)) = gv[u];
-                    }
-                    __syncthreads();
-                }
-                /* compact the slots' keys into the stage (m <= RES_SEL_MAX) */
-                if (tid < nsl) {
-                    const uint32_t o = s_so[tid];
-                    for (uint32_t k = 0; k < cnt_s; ++k) stage[o + k] = G[tid * RES_SLOT + 2 + k];
-                }
+                for (int u = 0; u < 2; ++u)
+                    if (tid + u * CT < m) stage[tid + u * CT] = kv[u];
                 __syncthreads();
                 WTP_PROBE(5);
                 /* ---- the ranks among the staged keys (buckets ba..bb; buckets between are empty:
@@ -1868,16 +1847,6 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader*
         res_body<true>(t, sd, head, qv, cand, res, thr_out, base, len, raw, lsub, wred, wstage);
     else
         res_body<false>(t, sd, head, qv, cand, res, thr_out, base, len, raw, lsub, wred, wstage);
-    {   /* clear this workgroup's slice of the idle region (the previous launch's; the next launch
-         * works in it), off the path: every read of the parity region of this launch is its own */
-        uint4* idle = reinterpret_cast<uint4*>(sel_region(head, parity_late(qv) ^ 1u));
-        constexpr int NV4 = (int)(SEL_REGION / 16);
-        const int per = (NV4 + (int)gridDim.x - 1) / (int)gridDim.x;
-        for (int i = threadIdx.x; i < per; i += RES_THREADS) {
-            const int j = (int)blockIdx.x * per + i;
-            if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
-        }
-    }
     if (t.stamps) { /* measurement only: the workgroup's end, once its stores have completed */
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();

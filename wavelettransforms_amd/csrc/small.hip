@@ -53,15 +53,6 @@ constexpr int SM_PF = 8; /* inverse-window words per thread prefetched in regist
  * above the bin, then up to SM_SLOT_KEYS keys */
 constexpr int SM_SLOT_KEYS = SM_SLOT_WORDS - 3;
 constexpr int SM_GATHER = SM_SEG_WG_MAX * SM_SLOT_WORDS; /* LDS words of the gathered slots (arena tail) */
-/* the publication ahead of barrier 0: every workgroup publishes its keys of the SM_PUB_BINS
- * 12-bit bins around its local estimate of the rank's bin, bin b in slot b % SM_PUB_BINS of its
- * region (SM_SLOT_WORDS words: tag, bin, count (bit 31: more than fit), smallest local key above
- * the bin, padding zeros, keys), drained by barrier 0's arrival; after barrier 0 the rank's bin d1
- * names ONE slot per workgroup, read in one round trip -- no slot round, no barrier 1, no
- * gather.  A workgroup whose window missed d1 sends the segment down the slot-round path. */
-constexpr int SM_PUB_BINS = SM_PUB_BINS_HOST;
-constexpr int SM_PUB_KEYS = SM_SLOT_WORDS - 5;
-static_assert(SM_PUB_KEYS <= SM_SLOT_KEYS, "a published slot fits the gather layout");
 static_assert(SM_GATHER == 8192, "small_geom.h's sm_inv_words reserves 8192 words for the gathered slots");
 
 /* per-segment selection state in the parity region (zero at the start of the launch) */
@@ -77,15 +68,6 @@ struct alignas(128) SmallState {
 static_assert(SM_MAX_SEG * sizeof(SmallState) <= SEG_PER_LAUNCH * sizeof(SelState), "small state fits the region");
 
 __device__ __forceinline__ uint32_t sm_abs_key(float x) { return __float_as_uint(x) & 0x7FFFFFFFu; }
-/* the publication regions (SM_PUB_BINS slots each) of workgroups w0 .. w0 + n - 1, behind the
- * slot-round slots in the candidate area; 16-byte sc1 accesses through a buffer resource */
-constexpr int SM_PUB_REGION = SM_PUB_BINS * SM_SLOT_WORDS;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sm_pub_rsrc(uint32_t* slots, int w0, int n) {
-    const uint64_t a = reinterpret_cast<uint64_t>(slots + (int64_t)RES_MAX_WG * SM_SLOT_WORDS + (int64_t)w0 * SM_PUB_REGION);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, n * SM_PUB_REGION * 4,
-                                             0x00020000);
-}
 template <class T>
 __device__ __forceinline__ void sm_stc(T* p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -317,16 +299,23 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     __shared__ uint32_t s_bef[2];
     __shared__ float staps[4][SM_F_MAX]; /* dec_lo, dec_hi, rec_lo, rec_hi */
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    /* the workspace parity by a VECTOR load, made uniform only once the level-0 window's loads have
-     * returned (its wait is then free): a scalar load of it is waited by the first LDS barrier and
-     * put a device round trip ahead of the window's loads */
-    const uint32_t qv = sm_ldc(&head->parity);
+    const uint32_t q = head->parity;
     if (t.stamps && tid == 0) atomicMin(t.stamps, sm_ticks()); /* measurement only */
+    {   /* clear this workgroup's slice of the idle region (the previous launch's) */
+        uint4* idle = reinterpret_cast<uint4*>(sel_region(head, q ^ 1u));
+        constexpr int NV4 = (int)(SEL_REGION / 16);
+        const int per = (NV4 + (int)gridDim.x - 1) / (int)gridDim.x;
+        for (int i = tid; i < per; i += SM_THREADS) {
+            const int j = (int)blockIdx.x * per + i;
+            if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
     SM_PROBE(6);
     int si = 0;
 #pragma unroll
     for (int i = 1; i < SM_MAX_SEG; ++i) si += (int)blockIdx.x >= t.wg_begin[i];
     const SmallSeg& g = t.s[si];
+    SmallState* st = reinterpret_cast<SmallState*>(sel_region(head, q)) + si;
     const int F = FT ? FT : t.tp.F;
     const int L = g.L;
     const int lt = (int)blockIdx.x - g.wg_begin;
@@ -400,18 +389,6 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                 const int e = e0 + tid + u * SM_THREADS;
                 if (e < n) X[e] = v[u];
             }
-        }
-    }
-    uint32_t q;
-    asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(q) : "v"(qv) : "memory");
-    SmallState* st = reinterpret_cast<SmallState*>(sel_region(head, q)) + si;
-    {   /* clear this workgroup's slice of the idle region (the previous launch's) */
-        uint4* idle = reinterpret_cast<uint4*>(sel_region(head, q ^ 1u));
-        constexpr int NV4 = (int)(SEL_REGION / 16);
-        const int per = (NV4 + (int)gridDim.x - 1) / (int)gridDim.x;
-        for (int i = tid; i < per; i += SM_THREADS) {
-            const int j = (int)blockIdx.x * per + i;
-            if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
         }
     }
     __syncthreads();
@@ -540,77 +517,6 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     }
     for (int i = tid; i < 4096; i += SM_THREADS)
         if (hist[i]) atomicAdd(&st->h1[i], hist[i]);
-    /* ---- publication (module comment at SM_PUB_BINS), ahead of barrier 0's arrival (whose drain
-     * then covers it: a workgroup past barrier 0 may read every slot of its segment): the local
-     * estimate of the rank's bin from this tile's histogram, its window of bins, the keys of the
-     * window bucketed into LDS slots, stored write-through */
-    const uint32_t tag = RES_SLOT_TAG | (q & ~RES_SLOT_TAG);
-    __shared__ int s_plo;
-    __shared__ uint32_t s_pfill[SM_PUB_BINS], s_pbmin[SM_PUB_BINS + 1];
-    uint32_t* PS = reinterpret_cast<uint32_t*>(arena + SM_ARENA - SM_GATHER); /* LDS slots (the gather area) */
-    {
-        /* the local bin of rank q (n - 1) over this tile's nloc keys */
-        constexpr int PB = 4096 / SM_THREADS;
-        uint32_t c[PB], cs = 0;
-#pragma unroll
-        for (int u = 0; u < PB; ++u) { c[u] = hist[PB * tid + u]; cs += c[u]; }
-        uint32_t nloc;
-        const uint32_t ex = sm_scan(cs, wtot, &nloc);
-        const double qf = g.n > 1 ? (double)g.r0 / (double)(g.n - 1) : 0.0;
-        const uint32_t rl = (uint32_t)(qf * (double)(nloc ? nloc - 1 : 0));
-        uint32_t e = ex;
-#pragma unroll
-        for (int u = 0; u < PB; ++u) {
-            if (rl >= e && rl < e + c[u]) s_plo = min(max(PB * tid + u - SM_PUB_BINS / 2 + 1, 0), 4096 - SM_PUB_BINS);
-            e += c[u];
-        }
-        if (tid < SM_PUB_BINS) { s_pfill[tid] = 0u; s_pbmin[tid] = 0xFFFFFFFFu; }
-        if (tid == 0) s_pbmin[SM_PUB_BINS] = 0xFFFFFFFFu;
-        if (nloc == 0 && tid == 0) s_plo = 0;
-        __syncthreads();
-        const int plo = s_plo;
-        uint32_t mhi = 0xFFFFFFFFu;
-        for (int i = tid; i < nkeys; i += SM_THREADS) {
-            const uint32_t k = K[i];
-            const int bi = (int)(k >> 19) - plo;
-            if (bi >= 0 && bi < SM_PUB_BINS) {
-                const uint32_t p = atomicAdd(&s_pfill[bi], 1u);
-                if (p < (uint32_t)SM_PUB_KEYS) PS[bi * SM_SLOT_WORDS + 5 + p] = k;
-                atomicMin(&s_pbmin[bi], k);
-            } else if (bi >= SM_PUB_BINS) {
-                mhi = min(mhi, k);
-            }
-        }
-        mhi = sm_wave_min(mhi);
-        if (lane == 0 && mhi != 0xFFFFFFFFu) atomicMin(&s_pbmin[SM_PUB_BINS], mhi);
-        __syncthreads();
-        if (tid < SM_PUB_BINS) { /* the slot header: tag, bin, count, smallest key above the bin, zeros */
-            uint32_t above = 0xFFFFFFFFu;
-            for (int j = tid + 1; j <= SM_PUB_BINS; ++j) above = min(above, s_pbmin[j]);
-            const uint32_t f = s_pfill[tid];
-            uint32_t* h = PS + tid * SM_SLOT_WORDS;
-            h[0] = tag;
-            h[1] = (uint32_t)(plo + tid);
-            h[2] = min(f, (uint32_t)SM_PUB_KEYS) | (f > (uint32_t)SM_PUB_KEYS ? 0x80000000u : 0u);
-            h[3] = above;
-            h[4] = (npad && plo + tid == 0) ? npad : 0u;
-        }
-        __syncthreads();
-    }
-    { /* one 16-byte granule per thread, only the granules a slot fills */
-        const int sl = tid / (SM_SLOT_WORDS / 4), gi = tid % (SM_SLOT_WORDS / 4);
-        static_assert(SM_PUB_BINS * SM_SLOT_WORDS / 4 <= SM_THREADS, "a granule per thread");
-        if (sl < SM_PUB_BINS) {
-            const uint32_t f = min(s_pfill[sl], (uint32_t)SM_PUB_KEYS);
-            if (4 * gi < 5 + (int)f) {
-                typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-                const u4v v = *reinterpret_cast<const u4v*>(PS + sl * SM_SLOT_WORDS + 4 * gi);
-                const int slot = (s_plo + sl) & (SM_PUB_BINS - 1);
-                __builtin_amdgcn_raw_buffer_store_b128(v, sm_pub_rsrc(t.slots, (int)blockIdx.x, 1),
-                                                       4 * (slot * SM_SLOT_WORDS + 4 * gi), 0, 16);
-            }
-        }
-    }
     const uint32_t nwg = (uint32_t)g.nwg;
     const uint32_t a0 = sm_arrive(&st->bar[0][0]);
     SM_PROBE(10);
@@ -685,7 +591,6 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     __shared__ uint32_t s_fill, s_min[2];
     bool ovf = false;
     uint32_t* G = reinterpret_cast<uint32_t*>(arena + SM_ARENA - SM_GATHER);
-    bool direct = false; /* the rank's bin came from the publication: no slot round */
     if (ok) {
         /* digit 1: the 12-bit bin of ra */
         if (tid == 0) { s_fill = 0; s_min[0] = 0xFFFFFFFFu; s_min[1] = 0xFFFFFFFFu; }
@@ -693,57 +598,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
         d1 = (uint32_t)s_dig[0];
         rem = ra0 - s_bef[0];
         SM_PROBE(2);
-        /* the published slot of bin d1 of every workgroup of the segment, in ONE round trip with
-         * the inverse's window prefetch, staged in the gather layout of the slot round below
-         * ([count | overflow, zeros, smallest key above the bin, keys]) */
-        {
-            __shared__ uint32_t s_miss;
-            if (tid == 0) s_miss = 0u;
-            __syncthreads();
-            {
-                typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-                constexpr int GW = SM_SLOT_WORDS / 4, GP = SM_GATHER / 4 / SM_THREADS;
-                const int ng = (int)nwg * GW, sl = (int)(d1 & (SM_PUB_BINS - 1));
-                const __amdgpu_buffer_rsrc_t prs = sm_pub_rsrc(t.slots, g.wg_begin, (int)nwg);
-                u4v pg[GP];
-#pragma unroll
-                for (int u = 0; u < GP; ++u) {
-                    const int i = min(tid + u * SM_THREADS, ng - 1), w = i / GW, gi = i - w * GW;
-                    pg[u] = __builtin_amdgcn_raw_buffer_load_b128(prs, 4 * (w * SM_PUB_REGION + sl * SM_SLOT_WORDS + 4 * gi), 0, 16);
-                }
-                float pv[SM_PF];
-#pragma unroll
-                for (int u = 0; u < SM_PF; ++u) {
-                    const int e = tid + u * SM_THREADS;
-                    pv[u] = e < nwin ? sm_ldc(win_src(e)) : 0.0f;
-                }
-#pragma unroll
-                for (int u = 0; u < GP; ++u) {
-                    const int i = min(tid + u * SM_THREADS, ng - 1), w = i / GW, gi = i - w * GW;
-                    uint32_t* gw = G + w * SM_SLOT_WORDS;
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        const int pw = 4 * gi + c;
-                        const uint32_t x = pg[u][c];
-                        if (pw == 0) { if (x != tag) s_miss = 1u; }
-                        else if (pw == 1) { if (x != d1) s_miss = 1u; }
-                        else gw[pw == 2 ? 0 : (pw == 3 ? 2 : (pw == 4 ? 1 : pw - 2))] = x;
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < SM_PF; ++u) {
-                    const int e = tid + u * SM_THREADS;
-                    if (e < nwin) WIN[e] = pv[u];
-                }
-                for (int e = tid + SM_PF * SM_THREADS; e < nwin; e += SM_THREADS) WIN[e] = sm_ldc(win_src(e));
-            }
-            __syncthreads();
-            direct = !s_miss; /* block-uniform; every workgroup reads the same slots: segment-uniform */
-        }
-        SM_PROBE(7);
-    }
-    if (ok && !direct) {
-        /* the slot round: this workgroup's keys of that bin into its slot, its smallest key above the bin */
+        /* this workgroup's keys of that bin into its slot, its smallest key above the bin */
         uint32_t* slot = t.slots + (int64_t)blockIdx.x * SM_SLOT_WORDS;
         uint32_t mn = 0xFFFFFFFFu;
         for (int i = tid; i < nkeys; i += SM_THREADS) {
@@ -789,21 +644,19 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     if (ok) {
         /* every slot of the segment into LDS (and the segment's largest key, final since barrier 0) */
         mk = sm_ldc(&st->maxkey);
-        if (!direct) {
-            const uint32_t* segs = t.slots + (int64_t)g.wg_begin * SM_SLOT_WORDS;
-            const int nw = (int)nwg * SM_SLOT_WORDS;
-            constexpr int GPT = SM_GATHER / SM_THREADS;
-            uint32_t gv[GPT];
+        const uint32_t* segs = t.slots + (int64_t)g.wg_begin * SM_SLOT_WORDS;
+        const int nw = (int)nwg * SM_SLOT_WORDS;
+        constexpr int GPT = SM_GATHER / SM_THREADS;
+        uint32_t gv[GPT];
 #pragma unroll
-            for (int u = 0; u < GPT; ++u) {
-                const int i = tid + u * SM_THREADS;
-                gv[u] = i < nw ? sm_ldc(segs + i) : 0u;
-            }
+        for (int u = 0; u < GPT; ++u) {
+            const int i = tid + u * SM_THREADS;
+            gv[u] = i < nw ? sm_ldc(segs + i) : 0u;
+        }
 #pragma unroll
-            for (int u = 0; u < GPT; ++u) {
-                const int i = tid + u * SM_THREADS;
-                if (i < nw) G[i] = gv[u];
-            }
+        for (int u = 0; u < GPT; ++u) {
+            const int i = tid + u * SM_THREADS;
+            if (i < nw) G[i] = gv[u];
         }
         for (int i = tid; i < 1536; i += SM_THREADS) hist[i] = 0u; /* pass A bins, then pass B's */
         if (tid == 0) s_min[1] = 0xFFFFFFFFu;

@@ -196,15 +196,12 @@ constexpr int RES_LATE_PCT = 45;
 constexpr int RES_STG = 32;                         /* inside keys a thread may stage (of its 96; ~11 expected) */
 /* After the first segment barrier every workgroup publishes the keys of the (one or two)
  * buckets holding the segment's ranks in a slot of its own: word 0 the count, then the keys */
-/* one workgroup's published region in the candidate area: one slot of RES_SLOT words per bucket,
- * [tag, count, keys...] -- the tag (RES_SLOT_TAG | the launch's parity counter) tells this launch's
- * slots from older ones (an empty bucket writes nothing and keeps an older tag); keys and every
- * other layout that shares the area have bits 31..30 clear.  A reader takes the first RES_SLOT0
- * words of a slot in one round trip (RES_SLOT0 - 2 keys), the rest only for a fuller bucket. */
-constexpr int RES_SLOT = 32;
-constexpr int RES_SLOT0 = 16;
-constexpr uint32_t RES_SLOT_TAG = 0xC0000000u;
-constexpr int RES_PUB_WORDS = RES_NSUB * RES_SLOT;
+/* one workgroup's published region in the candidate area: its bucket offsets (RES_NSUB + 1 words,
+ * padded to 16 bytes), then its inside keys bucket-sorted (at most RES_STG per thread).  (Round 4
+ * measured fixed per-bucket slots read in one round trip instead: the 16-byte granules scattered
+ * over 1024 slots are partial-line write-through stores, k_resident 28.0 -> 30.5 us.) */
+constexpr int RES_PUB_KEYS = (RES_NSUB + 1 + 3) / 4 * 4;
+constexpr int RES_PUB_WORDS = RES_PUB_KEYS + RES_STG * RES_THREADS;
 constexpr int RES_WG_WORDS = RES_PUB_WORDS;
 constexpr int RES_SEL_MAX = 1024;                   /* keys the one-wave select takes (more: full scan) */
 constexpr uint32_t RES_TIMEOUT_DEFAULT_US = 200000; /* a wait this long means the grid is not co-resident */
@@ -225,7 +222,6 @@ void launch_resident(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_res
 constexpr int SM_MAX_SEG = 4;       /* tensors per call */
 constexpr int SM_SEG_WG_MAX = 128;  /* workgroups per tensor */
 constexpr int SM_SLOT_WORDS = 64;   /* per workgroup in the candidate region: the keys of the rank's bin */
-constexpr int SM_PUB_BINS_HOST = 32; /* = small.hip's SM_PUB_BINS: published bin slots per workgroup */
 constexpr int SM_ARENA = 34 * 1024; /* LDS words of a workgroup's arena (136 KB) */
 constexpr int SM_F_MAX = 20;        /* longest filter */
 constexpr int SM_LMAX = 10;         /* = SM_MAX_L of small_geom.h */
