@@ -73,6 +73,8 @@ def parse():
                     help="level-0 groups in the three-launch form instead of the one-launch k_resident")
     ap.add_argument("--no-interior", action="store_true",
                     help="run every filter-bank tile in the general kernel (wtp_set_interior(0); A/B only)")
+    ap.add_argument("--frame-general", action="store_true",
+                    help="run the frame of edge tiles in the general kernel (wtp_set_interior(1); A/B only)")
     ap.add_argument("--no-rocprof", action="store_true", help="skip the in-run rocprofv3 kernel-stats child")
     ap.add_argument("--profile-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
@@ -130,6 +132,8 @@ def rocprof_child(args, timeout=240):
         cmd.append("--no-resident")
     if args.no_interior:
         cmd.append("--no-interior")
+    if args.frame_general:
+        cmd.append("--frame-general")
     env = dict(os.environ, TMPDIR="/tmp")
     try:
         subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
@@ -254,6 +258,8 @@ def main():
         engine.set_resident(False)
     if args.no_interior:
         engine.set_interior(False)
+    elif args.frame_general:
+        engine.set_interior(1)
 
     # ---------------------------------------------------------------- workload
     if args.config == "cfg2":

@@ -188,9 +188,10 @@ unsigned wtp_set_resident_timeout_us(unsigned us);
  * Returns the previous mode (process-wide). */
 int wtp_set_pipeline(int mode);
 /* The filter-bank levels run their interior tiles (input window inside the image, full tile)
- * in kernels compiled without the edge forms, and the frame of edge tiles in the general
- * kernel; mode 0 runs every tile in the general kernel (identical results).  Returns the
- * previous mode (process-wide). */
+ * in kernels compiled without the edge forms.  Mode 2 (default): the frame of edge tiles in the
+ * same kernels' edge-capable form; mode 1: the frame in the general kernel; mode 0: every tile in
+ * the general kernel (identical results in every mode).  Returns the previous mode
+ * (process-wide). */
 int wtp_set_interior(int mode);
 #define WTP_PATH_SMALL 4 /* every tensor of the call ran in one launch (2-D transforms, small population) */
 /* measurement hook (bench.py): while set, every resident launch atomically lowers stamps_dev[0] to

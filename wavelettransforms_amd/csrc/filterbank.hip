@@ -312,7 +312,7 @@ __device__ __forceinline__ void frame_tile(int f, int tilesC, int r0, int nr, in
 struct FwdIntTaps {
     f2 t[SM_F_MAX];
 };
-#define WTP_FB_INT_WPE __attribute__((amdgpu_waves_per_eu(6)))
+#define WTP_FB_INT_WPE __attribute__((amdgpu_waves_per_eu(EDGE ? 5 : 6))) /* EDGE: room for the edge forms */
 
 template <int FT>
 __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGroup g, TapsT<FT> tp) {
@@ -529,7 +529,10 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
 /* One analysis level over the INTERIOR tiles of a group (FwdGroup geo: tr0/nTR/tc0/nTC): every
  * tile's input window lies inside the image and its float4 rows are aligned, every output is a
  * full-tile interior site (i < N: ascending taps), so none of k_fwd_level's edge forms is compiled
- * in -- the frame of edge tiles runs k_fwd_level.  Same sums in the same order (pywt's
+ * in.  EDGE: the same kernel over the FRAME of tiles around that rectangle (FwdArgs.frame's decode):
+ * the input tile gathered with the periodic (odd: repeat-last) extension as k_fwd_level loads it,
+ * pywt's split order (wrapped terms first, wt_ana_point) only in the waves holding an output site
+ * i >= N, stores masked to the level's extent.  Same sums in the same order (pywt's
  * ascending-tap interior form, every sum from 0 as pywt starts it, so even the sign of a zero
  * matches).  Instruction shape:
  *   column pass: a thread's column samples are read as PAIRS of consecutive rows into aligned
@@ -537,7 +540,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
  *   move), against the {lo[j], hi[j]} tap pair in one SGPR pair;
  *   row pass: as k_fwd_level's interior form; stores by buffer instructions whose row offset is a
  *   scalar (the row is wave-uniform) and column offset the lane's -- no 64-bit address math. */
-template <int FT>
+template <int FT, bool EDGE>
 __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup g, FwdIntTaps tp) {
     static_assert(FT > 0 && FT % 2 == 0, "specialised even filters");
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -550,17 +553,48 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
     const int item = gt / g.tiles;
     const FwdArgs& a = g.geo;
     const int tile = gt - item * g.tiles;
-    const int per = a.nTR * a.nTC;
-    const int b = tile / per, t2 = tile - b * per;
-    const int trr = t2 / a.nTC;
-    const int o0r = (a.tr0 + trr) * FR, o0c = (a.tc0 + t2 - trr * a.nTC) * FC;
+    int b, trow, tcol;
+    if constexpr (EDGE) {
+        const int per = a.tilesR * a.tilesC - a.nTR * a.nTC;
+        b = tile / per;
+        frame_tile(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, &trow, &tcol);
+    } else {
+        const int per = a.nTR * a.nTC;
+        b = tile / per;
+        const int t2 = tile - b * per, trr = t2 / a.nTC;
+        trow = a.tr0 + trr;
+        tcol = a.tc0 + t2 - trr * a.nTC;
+    }
+    const int o0r = trow * FR, o0c = tcol * FC;
     const int gr0 = 2 * o0r - FT / 2 + 1, gc0 = 2 * o0c - FT / 2 + 1;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const float* x = g.in[item] + (int64_t)b * a.in_bs;
     WTP_FPROBE(0);
-    /* 1. the input tile, whole float4 rows from the aligned column gc0 - S0; every load of a
-     *    thread in flight before its first LDS write */
-    {
+    /* 1. the input tile; every load of a thread in flight before its first LDS write */
+    if constexpr (EDGE) {
+        /* rows by wave (row index and extension are scalar work), columns by lane; clamped
+         * duplicates rewrite their own value */
+        constexpr int RW = (NRc + 3) / 4, CW = (NCc + 63) / 64;
+        int col[CW];
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            const int gc = gc0 + min(lane + 64 * c, NCc - 1);
+            col[c] = (gc >= 0 && gc < a.C) ? gc : ext_idx(gc, a.C);
+        }
+        float v[RW][CW];
+#pragma unroll
+        for (int k = 0; k < RW; ++k) {
+            const int gr = gr0 + min(wv + 4 * k, NRc - 1);
+            const float* xr = x + (int64_t)((gr >= 0 && gr < a.R) ? gr : ext_idx(gr, a.R)) * a.C;
+#pragma unroll
+            for (int c = 0; c < CW; ++c) v[k][c] = xr[col[c]];
+        }
+#pragma unroll
+        for (int k = 0; k < RW; ++k)
+#pragma unroll
+            for (int c = 0; c < CW; ++c) T[min(wv + 4 * k, NRc - 1) * TP + S0 + min(lane + 64 * c, NCc - 1)] = v[k][c];
+    } else {
+        /* whole float4 rows from the aligned column gc0 - S0 */
         constexpr int NE = NRc * W4, K = (NE + FB_THREADS - 1) / FB_THREADS;
         const float* x0 = x + (int64_t)gr0 * a.C + (gc0 - S0);
         float4 q[K];
@@ -591,12 +625,30 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
 #pragma unroll
             for (int m = 0; m < NP; ++m) P[m] = f2{col[(2 * m) * TP], col[(2 * m + 1) * TP]};
             auto smp = [&](int s) { return (s & 1) ? P[s >> 1].yy : P[s >> 1].xx; };
+            const int i0 = FT / 2 + 2 * (o0r + RH * h); /* the site of the item's first output row */
+            if (!EDGE || __all(i0 + 2 * (RH - 1) < a.R)) {
 #pragma unroll
-            for (int r = 0; r < RH; ++r) res[q][r] = f2{0.0f, 0.0f} + tp.t[0] * smp(2 * r + FT - 1);
+                for (int r = 0; r < RH; ++r) res[q][r] = f2{0.0f, 0.0f} + tp.t[0] * smp(2 * r + FT - 1);
 #pragma unroll
-            for (int j = 1; j < FT; ++j)
+                for (int j = 1; j < FT; ++j)
 #pragma unroll
-                for (int r = 0; r < RH; ++r) res[q][r] = res[q][r] + tp.t[j] * smp(2 * r + FT - 1 - j);
+                    for (int r = 0; r < RH; ++r) res[q][r] = res[q][r] + tp.t[j] * smp(2 * r + FT - 1 - j);
+            } else {
+                /* wt_ana_point's order: the wrapped terms (i - j >= N) by descending j, then the
+                 * rest ascending -- for a site i < N that is the ascending interior sum */
+#pragma unroll
+                for (int r = 0; r < RH; ++r) {
+                    const int i = i0 + 2 * r;
+                    f2 acc = {0.0f, 0.0f};
+#pragma unroll
+                    for (int j = FT - 1; j >= 0; --j)
+                        if (i - j >= a.R) acc = acc + tp.t[j] * smp(2 * r + FT - 1 - j);
+#pragma unroll
+                    for (int j = 0; j < FT; ++j)
+                        if (i - j < a.R) acc = acc + tp.t[j] * smp(2 * r + FT - 1 - j);
+                    res[q][r] = acc;
+                }
+            }
         }
     }
     __syncthreads(); /* every read of T is done: LH overwrites it */
@@ -621,6 +673,9 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
         const int pitchA = a.last ? a.PC : a.Co;
         const int voff = 4 * (o0c + lane);
         auto flo = [&](int k) { return (k & 1) ? tp.t[k >> 1].y : tp.t[k >> 1].x; };
+        const int ic = FT / 2 + 2 * (o0c + lane); /* the lane's output site along the row */
+        const bool cedge = EDGE && !__all(ic < a.C);
+        const bool cin = !EDGE || o0c + lane < a.Co;
         constexpr int NW = FB_THREADS / 64;
         static_assert(FR % (2 * NW) == 0, "row pairs per wave");
 #pragma unroll
@@ -634,19 +689,41 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
                 vB[j] = f2{xb.x, xb.y};
             }
             const f2 z2 = {0.0f, 0.0f};
-            f2 aA = z2 + flo(0) * vA[0], dA = z2 + flo(1) * vA[0], aB = z2 + flo(0) * vB[0], dB = z2 + flo(1) * vB[0];
+            f2 aA, dA, aB, dB;
+            if (!cedge) {
+                aA = z2 + flo(0) * vA[0];
+                dA = z2 + flo(1) * vA[0];
+                aB = z2 + flo(0) * vB[0];
+                dB = z2 + flo(1) * vB[0];
 #pragma unroll
-            for (int j = 1; j < FT; ++j) {
-                const float tl = flo(2 * j), th = flo(2 * j + 1);
-                aA = aA + tl * vA[j];
-                dA = dA + th * vA[j];
-                aB = aB + tl * vB[j];
-                dB = dB + th * vB[j];
+                for (int j = 1; j < FT; ++j) {
+                    const float tl = flo(2 * j), th = flo(2 * j + 1);
+                    aA = aA + tl * vA[j];
+                    dA = dA + th * vA[j];
+                    aB = aB + tl * vB[j];
+                    dB = dB + th * vB[j];
+                }
+            } else { /* wt_ana_point's split order where ic >= N, as the column pass */
+                aA = z2; dA = z2; aB = z2; dB = z2;
+                auto term = [&](int j) {
+                    const float tl = flo(2 * j), th = flo(2 * j + 1);
+                    aA = aA + tl * vA[j];
+                    dA = dA + th * vA[j];
+                    aB = aB + tl * vB[j];
+                    dB = dB + th * vB[j];
+                };
+#pragma unroll
+                for (int j = FT - 1; j >= 0; --j)
+                    if (ic - j >= a.C) term(j);
+#pragma unroll
+                for (int j = 0; j < FT; ++j)
+                    if (ic - j < a.C) term(j);
             }
             /* low = (aa, da), high = (ad, dd) */
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const int r = o0r + (u ? oB : oA);
+                if (EDGE && !(cin && r < a.Ro)) continue;
                 const f2 lw = u ? aB : aA, hg = u ? dB : dA;
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.x), rA, voff, 4 * r * pitchA, 0);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.x), rP, voff, 4 * (r * a.PC + a.offC), 0);
@@ -976,12 +1053,17 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
 /* One synthesis level over the INTERIOR tiles of a group (InvGroup geo: tr0/nTR/tc0/nTC): every
  * output of the tile is a full-tile non-special site whose coefficient window lies inside the
  * level (no wrap), so the tile's coefficient rows / columns are exactly IR/2 + H - (H & 1) and
- * only wt_syn_pass's ascending interior order occurs; the frame of edge tiles runs k_inv_level.
+ * only wt_syn_pass's ascending interior order occurs.  EDGE: the same kernel over the FRAME of tiles
+ * around that rectangle (InvArgs.frame's decode; the host runs it when the level is at least a
+ * window tall and wide, so one wrap brings every coefficient position into range): the window
+ * loaded with the periodic wrap, wt_syn_pass's special / wrapped-first orders only where a site
+ * needs them (the samples and taps are the interior ones -- unwrapped positions stay monotonic),
+ * stores and zero counts masked to the output extent.
  * Same sums in the same order as k_inv_level's interior forms (from 0, as pywt).  Instruction shape: coefficient loads are buffer loads
  * whose four subband offsets are scalars (one lane offset per element), the row pass's per-lane
  * taps are register pairs broadcast by op_sel, the output stores take the row as a scalar
  * offset, and zeros are counted by ballot. */
-template <int FT>
+template <int FT, bool EDGE>
 __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup g, SmallTaps tp) {
     static_assert(FT > 0 && FT % 2 == 0, "specialised even filters");
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -991,10 +1073,20 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
     const int item = gt / g.tiles;
     const InvArgs& a = g.geo;
     const int tile = gt - item * g.tiles;
-    const int per = a.nTR * a.nTC;
-    const int b = tile / per, t2 = tile - b * per;
-    const int trr = t2 / a.nTC;
-    const int n0 = (a.tr0 + trr) * IR, m0 = (a.tc0 + t2 - trr * a.nTC) * IC;
+    int b, trow, tcol;
+    if constexpr (EDGE) {
+        const int per = a.tilesR * a.tilesC - a.nTR * a.nTC;
+        b = tile / per;
+        frame_tile(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, &trow, &tcol);
+    } else {
+        const int per = a.nTR * a.nTC;
+        b = tile / per;
+        const int t2 = tile - b * per, trr = t2 / a.nTC;
+        trow = a.tr0 + trr;
+        tcol = a.tc0 + t2 - trr * a.nTC;
+    }
+    const int n0 = trow * IR, m0 = tcol * IC;
+    const int nl = min(n0 + IR, a.outH) - 1, ml = min(m0 + IC, a.outW) - 1; /* EDGE: the last stored output */
     const int r_lo = site_u(n0, a.R, FT).iu - H + 1, c_lo = site_u(m0, a.C, FT).iu - H + 1;
     float2* Aq = reinterpret_cast<float2*>(lds); /* (cA, cH=da) */
     float2* Dq = Aq + NR * NC;                   /* (cV=ad, cD=dd) */
@@ -1018,7 +1110,11 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
         for (int k = 0; k < K; ++k) {
             const int e = min(k * FB_THREADS + (int)threadIdx.x, NE - 1);
             const int rr = e / NC, cc = e - rr * NC;
-            const int r = r_lo + rr, c = c_lo + cc;
+            int r = r_lo + rr, c = c_lo + cc;
+            if constexpr (EDGE) { /* one wrap suffices: the level is at least NR x NC */
+                r = r < 0 ? r + a.R : (r >= a.R ? r - a.R : r);
+                c = c < 0 ? c + a.C : (c >= a.C ? c - a.C : c);
+            }
             const int vo = 4 * (r * a.PC + c);
             const int va = a.a_from_P ? vo : 4 * (r * a.lda + c);
             q[k].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rA, va, 0, 0));
@@ -1050,6 +1146,17 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
          * two sums are independent chains that interleave */
         constexpr int PE1 = (H & 1) ? 0 : 1, NS = HM + PE1;
         constexpr int PAR0 = (H & 1) ? 0 : 1, PAR1 = 1 - PAR0;
+        /* EDGE: the sites of the lane's two outputs and their order rule -- wt_syn_pass adds the
+         * terms with i - j >= T by descending j first (T = 0 at a special site, N past the end),
+         * then the others ascending; an interior site (i < N, T = N) has no first-loop term */
+        int i0 = 0, i1 = 0, T0 = 0, T1 = 0;
+        bool redge = false;
+        if constexpr (EDGE) {
+            const SiteU s0 = site_u(m0 + 2 * c, a.C, FT), s1 = site_u(m0 + 2 * c + 1, a.C, FT);
+            i0 = s0.i; T0 = s0.special ? 0 : a.C;
+            i1 = s1.i; T1 = s1.special ? 0 : a.C;
+            redge = __any(s0.special || s0.i >= a.C || s1.special || s1.i >= a.C);
+        }
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
             const int row = min(2 * (wv + 4 * k) + ro, NR - 1);
@@ -1061,18 +1168,41 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
 #pragma unroll
             for (int q = 0; q < NS; ++q) { const float2 t = pa[q]; v[q] = f2{t.x, t.y}; }
             const f2 z2 = {0.0f, 0.0f};
-            f2 a0 = z2 + tp.f[2][PAR0] * sp(0, 0), a1 = z2 + tp.f[2][PAR1] * sp(1, 0);
+            f2 a0, a1;
+            if (!redge) {
+                a0 = z2 + tp.f[2][PAR0] * sp(0, 0);
+                a1 = z2 + tp.f[2][PAR1] * sp(1, 0);
 #pragma unroll
-            for (int j = 1; j < HM; ++j) {
-                a0 = a0 + tp.f[2][2 * j + PAR0] * sp(0, j);
-                a1 = a1 + tp.f[2][2 * j + PAR1] * sp(1, j);
-            }
+                for (int j = 1; j < HM; ++j) {
+                    a0 = a0 + tp.f[2][2 * j + PAR0] * sp(0, j);
+                    a1 = a1 + tp.f[2][2 * j + PAR1] * sp(1, j);
+                }
 #pragma unroll
-            for (int q = 0; q < NS; ++q) { const float2 t = pd[q]; v[q] = f2{t.x, t.y}; }
+                for (int q = 0; q < NS; ++q) { const float2 t = pd[q]; v[q] = f2{t.x, t.y}; }
 #pragma unroll
-            for (int j = 0; j < HM; ++j) {
-                a0 = a0 + tp.f[3][2 * j + PAR0] * sp(0, j);
-                a1 = a1 + tp.f[3][2 * j + PAR1] * sp(1, j);
+                for (int j = 0; j < HM; ++j) {
+                    a0 = a0 + tp.f[3][2 * j + PAR0] * sp(0, j);
+                    a1 = a1 + tp.f[3][2 * j + PAR1] * sp(1, j);
+                }
+            } else {
+                a0 = z2;
+                a1 = z2;
+                auto pass = [&](const float* rec) {
+#pragma unroll
+                    for (int j = HM - 1; j >= 0; --j) {
+                        if (i0 - j >= T0) a0 = a0 + rec[2 * j + PAR0] * sp(0, j);
+                        if (i1 - j >= T1) a1 = a1 + rec[2 * j + PAR1] * sp(1, j);
+                    }
+#pragma unroll
+                    for (int j = 0; j < HM; ++j) {
+                        if (i0 - j < T0) a0 = a0 + rec[2 * j + PAR0] * sp(0, j);
+                        if (i1 - j < T1) a1 = a1 + rec[2 * j + PAR1] * sp(1, j);
+                    }
+                };
+                pass(tp.f[2]);
+#pragma unroll
+                for (int q = 0; q < NS; ++q) { const float2 t = pd[q]; v[q] = f2{t.x, t.y}; }
+                pass(tp.f[3]);
             }
             /* computed HERE: without this the compiler sinks the sums past the barrier below
              * (their only use is the LoHi write) and keeps every sample alive across it */
@@ -1105,37 +1235,75 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
     float2 r[NV];
 #pragma unroll
     for (int q = 0; q < NV; ++q) r[q] = LoHi[(g0 + q) * IC + lane];
-    f2 acc[RB2];
-#pragma unroll
-    for (int j = 0; j < H; ++j) {
-        const float t0 = tp.f[2][2 * j], t1 = tp.f[2][2 * j + 1];
-#pragma unroll
-        for (int k = 0; k < RB2; ++k) {
-            const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
-            const float t = par ? t1 : t0;
-            const f2 p = f2{t, t} * f2{r[base - j].x, r[base - j + RB2 / 2].x};
-            acc[k] = (j == 0 ? f2{0.0f, 0.0f} : acc[k]) + p;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < H; ++j) {
-        const float t0 = tp.f[3][2 * j], t1 = tp.f[3][2 * j + 1];
-#pragma unroll
-        for (int k = 0; k < RB2; ++k) {
-            const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
-            const float t = par ? t1 : t0;
-            acc[k] = acc[k] + f2{t, t} * f2{r[base - j].y, r[base - j + RB2 / 2].y};
-        }
-    }
     const __amdgpu_buffer_rsrc_t rY =
         __builtin_amdgcn_make_buffer_rsrc(g.y[item] + (int64_t)b * a.outH * a.outW, 0, 4 * a.outH * a.outW, 0x00020000);
     const int vy = 4 * m;
     uint32_t z = 0; /* wave-uniform: zeros of this wave's outputs */
+    bool cedge = false;
+    if constexpr (EDGE) {
+        /* a block holding a special or wrapped site (or outputs past the extent) runs its rows one
+         * by one in wt_syn_pass's order; the row's site is wave-uniform, so are the branches */
+        for (int k = 0; k < RB; ++k) {
+            const SiteU s = site_u(nf + k, a.R, FT);
+            cedge |= s.special || s.i >= a.R || nf + k > nl;
+        }
+    }
+    if (cedge) {
+        const bool min_ = m <= ml;
 #pragma unroll
-    for (int k = 0; k < RB2; ++k) {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[k].x), rY, vy, 4 * (nf + k) * a.outW, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[k].y), rY, vy, 4 * (nf + k + RB2) * a.outW, 0);
-        z += (uint32_t)__popcll(__ballot(acc[k].x == 0.0f)) + (uint32_t)__popcll(__ballot(acc[k].y == 0.0f));
+        for (int k = 0; k < RB; ++k) {
+            const int n = nf + k;
+            const SiteU s = site_u(n, a.R, FT);
+            const int Tn = s.special ? 0 : a.R;
+            const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
+            float y = 0.0f;
+#pragma unroll
+            for (int pass = 0; pass < 2; ++pass) {
+                const float* rec = tp.f[2 + pass];
+#pragma unroll
+                for (int j = H - 1; j >= 0; --j)
+                    if (s.i - j >= Tn) y = y + rec[2 * j + par] * (pass ? r[base - j].y : r[base - j].x);
+#pragma unroll
+                for (int j = 0; j < H; ++j)
+                    if (s.i - j < Tn) y = y + rec[2 * j + par] * (pass ? r[base - j].y : r[base - j].x);
+            }
+            if (n <= nl) {
+                if (min_) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), rY, vy, 4 * n * a.outW, 0);
+                z += (uint32_t)__popcll(__ballot(min_ && y == 0.0f));
+            }
+        }
+    } else {
+        f2 acc[RB2];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            const float t0 = tp.f[2][2 * j], t1 = tp.f[2][2 * j + 1];
+#pragma unroll
+            for (int k = 0; k < RB2; ++k) {
+                const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
+                const float t = par ? t1 : t0;
+                const f2 p = f2{t, t} * f2{r[base - j].x, r[base - j + RB2 / 2].x};
+                acc[k] = (j == 0 ? f2{0.0f, 0.0f} : acc[k]) + p;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            const float t0 = tp.f[3][2 * j], t1 = tp.f[3][2 * j + 1];
+#pragma unroll
+            for (int k = 0; k < RB2; ++k) {
+                const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
+                const float t = par ? t1 : t0;
+                acc[k] = acc[k] + f2{t, t} * f2{r[base - j].y, r[base - j + RB2 / 2].y};
+            }
+        }
+        const bool min_ = !EDGE || m <= ml; /* EDGE: a partial last tile column */
+#pragma unroll
+        for (int k = 0; k < RB2; ++k) {
+            if (min_) {
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[k].x), rY, vy, 4 * (nf + k) * a.outW, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[k].y), rY, vy, 4 * (nf + k + RB2) * a.outW, 0);
+            }
+            z += (uint32_t)__popcll(__ballot(min_ && acc[k].x == 0.0f)) + (uint32_t)__popcll(__ballot(min_ && acc[k].y == 0.0f));
+        }
     }
     if (a.zc) {
         /* 8 bytes: the dynamic LDS follows the static variables, and a 4-byte one would leave
@@ -1152,10 +1320,11 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
 }
 
 /* ------------------------------------------------------------ launchers --- */
-/* interior tiles in their own kernels (k_fwd_int): on by default; 0 runs every tile in
- * k_fwd_level (A/B and parity cross-checks) */
-static std::atomic<int> g_fb_interior{1};
-int fb_set_interior(int mode) { return g_fb_interior.exchange(mode ? 1 : 0); }
+/* which kernels run a level's tiles: 2 (default) the interior rectangle in k_fwd_int / k_inv_int and
+ * the frame around it in their EDGE forms; 1 the frame in the general k_fwd_level / k_inv_level;
+ * 0 every tile in the general kernels (A/B and parity cross-checks) */
+static std::atomic<int> g_fb_interior{2};
+int fb_set_interior(int mode) { return g_fb_interior.exchange(mode < 0 ? 0 : (mode > 2 ? 2 : mode)); }
 
 
 /* dynamic LDS per workgroup; `alias`: the specialised kernels write their second-pass input
@@ -1190,12 +1359,12 @@ static void fwd_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
     static_assert(FT <= SM_F_MAX, "SmallTaps holds the specialised filters");
     hipLaunchKernelGGL(k_fwd_level<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, FT > 0), s, g, taps_of<FT>(tp));
 }
-template <int FT>
+template <int FT, bool EDGE>
 static void fwd_int_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
     FwdIntTaps t;
     memset(&t, 0, sizeof t);
     for (int j = 0; j < FT; ++j) t.t[j] = f2{tp.f[0][j], tp.f[1][j]};
-    hipLaunchKernelGGL(k_fwd_int<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, true), s, g, t);
+    hipLaunchKernelGGL((k_fwd_int<FT, EDGE>), dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, true), s, g, t);
 }
 
 /* The interior rectangle of a forward level's tile grid (k_fwd_int's tiles): a tile row is
@@ -1225,9 +1394,9 @@ template <int FT>
 static void inv_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
     hipLaunchKernelGGL(k_inv_level<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F, FT > 0), s, g, taps_of<FT>(tp));
 }
-template <int FT>
+template <int FT, bool EDGE>
 static void inv_int_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
-    hipLaunchKernelGGL(k_inv_int<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F, true), s, g, taps_of<FT>(tp));
+    hipLaunchKernelGGL((k_inv_int<FT, EDGE>), dim3(grid), dim3(FB_THREADS), inv_lds(tp.F, true), s, g, taps_of<FT>(tp));
 }
 
 /* The interior rectangle of a synthesis level's tile grid (k_inv_int's tiles): along each axis a
@@ -1255,6 +1424,11 @@ static bool inv_interior(const InvArgs& a, int F, int* r0, int* nr, int* c0, int
     if ((int64_t)4 * a.P_bs > INT32_MAX || (int64_t)4 * a.outH * a.outW > INT32_MAX) return false;
     if (!a.a_from_P && (int64_t)4 * a.a_bs > INT32_MAX) return false;
     return inv_axis(a.tilesR, IR, a.outH, a.R, F, r0, nr) && inv_axis(a.tilesC, IC, a.outW, a.C, F, c0, nc);
+}
+/* k_inv_int's EDGE form wraps a window coordinate once: the level spans a whole window */
+static bool inv_frame_ok(const InvArgs& a, int F) {
+    const int H = F / 2, NR = IR / 2 + H - (H & 1), NC = IC / 2 + H - (H & 1);
+    return a.R >= NR && a.C >= NC;
 }
 
 /* The tiled path needs an even filter, the LDS budget, and images large enough that a tile
@@ -1354,16 +1528,17 @@ static void fwd_general(const FwdGroup& g, int grid, const Taps& tp, hipStream_t
     default: fwd_go<0>(g, grid, tp, s); break;
     }
 }
+template <bool EDGE>
 static void fwd_interior_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
     switch (tp.F) {
-    case 2: fwd_int_go<2>(g, grid, tp, s); break;
-    case 4: fwd_int_go<4>(g, grid, tp, s); break;
-    case 6: fwd_int_go<6>(g, grid, tp, s); break;
-    case 8: fwd_int_go<8>(g, grid, tp, s); break;
-    case 10: fwd_int_go<10>(g, grid, tp, s); break;
-    case 12: fwd_int_go<12>(g, grid, tp, s); break;
-    case 16: fwd_int_go<16>(g, grid, tp, s); break;
-    case 18: fwd_int_go<18>(g, grid, tp, s); break;
+    case 2: fwd_int_go<2, EDGE>(g, grid, tp, s); break;
+    case 4: fwd_int_go<4, EDGE>(g, grid, tp, s); break;
+    case 6: fwd_int_go<6, EDGE>(g, grid, tp, s); break;
+    case 8: fwd_int_go<8, EDGE>(g, grid, tp, s); break;
+    case 10: fwd_int_go<10, EDGE>(g, grid, tp, s); break;
+    case 12: fwd_int_go<12, EDGE>(g, grid, tp, s); break;
+    case 16: fwd_int_go<16, EDGE>(g, grid, tp, s); break;
+    case 18: fwd_int_go<18, EDGE>(g, grid, tp, s); break;
     default: break;
     }
 }
@@ -1380,16 +1555,17 @@ static void inv_general(const InvGroup& g, int grid, const Taps& tp, hipStream_t
     default: inv_go<0>(g, grid, tp, s); break;
     }
 }
+template <bool EDGE>
 static void inv_interior_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
     switch (tp.F) {
-    case 2: inv_int_go<2>(g, grid, tp, s); break;
-    case 4: inv_int_go<4>(g, grid, tp, s); break;
-    case 6: inv_int_go<6>(g, grid, tp, s); break;
-    case 8: inv_int_go<8>(g, grid, tp, s); break;
-    case 10: inv_int_go<10>(g, grid, tp, s); break;
-    case 12: inv_int_go<12>(g, grid, tp, s); break;
-    case 16: inv_int_go<16>(g, grid, tp, s); break;
-    case 18: inv_int_go<18>(g, grid, tp, s); break;
+    case 2: inv_int_go<2, EDGE>(g, grid, tp, s); break;
+    case 4: inv_int_go<4, EDGE>(g, grid, tp, s); break;
+    case 6: inv_int_go<6, EDGE>(g, grid, tp, s); break;
+    case 8: inv_int_go<8, EDGE>(g, grid, tp, s); break;
+    case 10: inv_int_go<10, EDGE>(g, grid, tp, s); break;
+    case 12: inv_int_go<12, EDGE>(g, grid, tp, s); break;
+    case 16: inv_int_go<16, EDGE>(g, grid, tp, s); break;
+    case 18: inv_int_go<18, EDGE>(g, grid, tp, s); break;
     default: break;
     }
 }
@@ -1417,20 +1593,24 @@ void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) 
             g.P[m] = args[grp[m]].P;
         }
         int r0, nr, c0, nc;
-        if (g_fb_interior.load(std::memory_order_relaxed) && fwd_int_filter(tp.F) &&
-            fwd_interior(g.geo, tp.F, &r0, &nr, &c0, &nc)) {
-            /* the interior tiles in k_fwd_int, then the frame around them in k_fwd_level (measured
-             * in round 4: the frame on a stream of its own beside the interior launch gained
-             * nothing -- both launches fill every CU, so the work only moved) */
+        const int mode = g_fb_interior.load(std::memory_order_relaxed);
+        if (mode && fwd_int_filter(tp.F) && fwd_interior(g.geo, tp.F, &r0, &nr, &c0, &nc)) {
+            /* the interior tiles in k_fwd_int, then the frame around them (measured in round 4:
+             * the frame on a stream of its own beside the interior launch gained nothing -- both
+             * launches fill every CU, so the work only moved) */
             const int B = g.tiles / (g.geo.tilesR * g.geo.tilesC);
             g.geo.tr0 = r0; g.geo.nTR = nr; g.geo.tc0 = c0; g.geo.nTC = nc;
             FwdGroup gi = g;
             gi.tiles = nr * nc * B;
             const int fr = g.geo.tilesR * g.geo.tilesC - nr * nc;
-            fwd_interior_go(gi, gi.n * gi.tiles, tp, s);
+            fwd_interior_go<false>(gi, gi.n * gi.tiles, tp, s);
             if (fr == 0) continue;
             g.geo.frame = 1;
             g.tiles = fr * B;
+            if (mode == 2) {
+                fwd_interior_go<true>(g, g.n * g.tiles, tp, s);
+                continue;
+            }
         }
         fwd_general(g, g.n * g.tiles, tp, s);
     }
@@ -1472,20 +1652,22 @@ void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s) 
             g.zc_off[m] = x.zc ? (int32_t)(x.zc - g.geo.zc) : 0;
         }
         int r0, nr, c0, nc;
-        if (g_fb_interior.load(std::memory_order_relaxed) && fwd_int_filter(tp.F) &&
-            inv_interior(g.geo, tp.F, &r0, &nr, &c0, &nc)) {
-            /* the interior tiles in k_inv_int, then the frame around them in k_inv_level (measured
-             * in round 4: the frame on a stream of its own beside the interior launch gained
-             * nothing -- both launches fill every CU, so the work only moved) */
+        const int mode = g_fb_interior.load(std::memory_order_relaxed);
+        if (mode && fwd_int_filter(tp.F) && inv_interior(g.geo, tp.F, &r0, &nr, &c0, &nc)) {
+            /* the interior tiles in k_inv_int, then the frame around them (as the analysis) */
             const int B = g.tiles / (g.geo.tilesR * g.geo.tilesC);
             g.geo.tr0 = r0; g.geo.nTR = nr; g.geo.tc0 = c0; g.geo.nTC = nc;
             InvGroup gi = g;
             gi.tiles = nr * nc * B;
             const int fr = g.geo.tilesR * g.geo.tilesC - nr * nc;
-            inv_interior_go(gi, gi.n * gi.tiles, tp, s);
+            inv_interior_go<false>(gi, gi.n * gi.tiles, tp, s);
             if (fr == 0) continue;
             g.geo.frame = 1;
             g.tiles = fr * B;
+            if (mode == 2 && inv_frame_ok(g.geo, tp.F)) {
+                inv_interior_go<true>(g, g.n * g.tiles, tp, s);
+                continue;
+            }
         }
         inv_general(g, g.n * g.tiles, tp, s);
     }

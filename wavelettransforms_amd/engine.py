@@ -228,9 +228,11 @@ def set_pipeline(enabled):
 
 
 def set_interior(enabled):
-    """Run the filter-bank levels' interior tiles in their edge-free kernels (default) or every
-    tile in the general kernel (include/wtprune.h wtp_set_interior); returns the previous setting."""
-    return bool(N.lib().wtp_set_interior(1 if enabled else 0))
+    """Filter-bank kernel choice (include/wtprune.h wtp_set_interior): True / 2 the interior tiles
+    and the frame around them in the edge-free kernels and their edge form (default), 1 the frame
+    in the general kernel, False / 0 every tile in the general kernel; returns the previous mode."""
+    mode = (2 if enabled else 0) if isinstance(enabled, bool) else int(enabled)
+    return int(N.lib().wtp_set_interior(mode))
 
 
 def resident_capacity():
