@@ -417,44 +417,24 @@ __device__ __forceinline__ void window_search_wave(const SegDesc& sd, const uint
  * in the thread's own LDS column (stage[i * CT + tid], conflict-free, no scan).  A thread may
  * stage up to STG of its 4*IT keys; more sends the segment to the full-scan select. */
 constexpr int STG = 24;
-template <int CT, int IT, bool FULL, bool WIN>
-__device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __restrict__ st,
-                                             uint32_t* __restrict__ cand, int64_t base, int len, bool first,
-                                             uint32_t* lsub, uint32_t* lbase, uint32_t* stage,
-                                             WindowLds<CT>* wl, uint32_t (*wred)[4], int* wtot) {
-    const float* p = sd.data + base;
-    WTP_CPROBE(0);
-    uint32_t kl, kh, sh;
-    float4 v[IT];
-    if constexpr (WIN) {
-        /* sample loads first, then the stream loads: the window is built while the chunk arrives */
-        uint32_t ks[M_SAMPLE / CT];
-        sample_keys<CT, M_SAMPLE>(sd, ks);
-        if (FULL) load_chunk<IT, CT>(p, v);
-        else load_chunk_ragged<IT, CT>(p, len, v);
-        window_from_keys<CT, M_SAMPLE>(sd, ks, *wl, &kl, &kh, &sh);
-        if (first && threadIdx.x == 0) { st->kl = kl; st->kh = kh; st->shift = sh; } /* for the select */
-    } else {
-        /* the window came from k_window; the stream loads go out first (the window words are
-         * scalar loads, counted separately from the vector loads) */
-        if (FULL) load_chunk<IT, CT>(p, v);
-        else load_chunk_ragged<IT, CT>(p, len, v);
-        kl = st->kl;
-        kh = st->kh;
-        sh = st->shift;
-    }
-    WTP_CPROBE(1);
-    const int nsub = 1 << sd.nsub_log2;
+
+/* the counting pass over a thread's IT float4 (element e of slot (it, c) is 4 (it CT + tid) + c;
+ * past len -- a ragged chunk -- nothing counts): below / equal-to-kl counts, the max key, and the
+ * inside keys staged in the thread's LDS column; clears the block's bucket histogram */
+template <int CT, int IT>
+__device__ __forceinline__ void collect_count(const float4 (&v)[IT], bool full, int len, int nsub, uint32_t kl,
+                                              uint32_t kh, uint32_t* lsub, uint32_t* stage, uint32_t& below,
+                                              uint32_t& eql, uint32_t& mx, uint32_t& cnt) {
     for (int i = threadIdx.x; i < nsub; i += CT) lsub[i] = 0;
     const uint32_t span = kh - kl; /* >= 1 */
-    uint32_t below = 0, eql = 0, mx = 0, cnt = 0;
+    below = 0; eql = 0; mx = 0; cnt = 0;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
         const int e = 4 * (it * CT + (int)threadIdx.x);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const uint32_t k = abs_key(f4_get(v[it], c));
-            const bool valid = FULL || e + c < len;
+            const bool valid = full || e + c < len;
             mx = max(mx, k); /* 0 past len: no effect */
             below += valid && k < kl;
             eql += valid && k == kl;
@@ -464,6 +444,17 @@ __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __rest
             }
         }
     }
+}
+
+/* the rest of a chunk: the block's counters into the segment's (8-way sharded agent atomics), the
+ * inside keys bucketed by key range (LDS histogram, the block's returning reservation atomics all
+ * in flight at once) and scattered into the candidate buckets */
+template <int CT>
+__device__ __forceinline__ void collect_finish(const SegDesc& sd, SelState* __restrict__ st, uint32_t* __restrict__ cand,
+                                               uint32_t kl, uint32_t sh, uint32_t below, uint32_t eql, uint32_t mx,
+                                               uint32_t cnt, uint32_t* lsub, uint32_t* lbase, uint32_t* stage,
+                                               uint32_t (*wred)[4], int* wtot) {
+    const int nsub = 1 << sd.nsub_log2;
     /* one block reduction for the counters */
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     {
@@ -522,6 +513,41 @@ __device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __rest
         if (at < bcap) out[(int64_t)b * bcap + at] = k; /* counted beyond capacity: the select sees it */
     }
     WTP_CPROBE(5);
+}
+
+/* One chunk of a k_collect_t block: its loads (and with WIN the window from the block's own
+ * sample), the counting pass, the rest.  FULL: a whole 16-byte-aligned chunk (unpredicated
+ * loads); otherwise a ragged or unaligned one (range-checked buffer loads). */
+template <int CT, int IT, bool FULL, bool WIN>
+__device__ __forceinline__ void collect_body(const SegDesc& sd, SelState* __restrict__ st,
+                                             uint32_t* __restrict__ cand, int64_t base, int len, bool first,
+                                             uint32_t* lsub, uint32_t* lbase, uint32_t* stage,
+                                             WindowLds<CT>* wl, uint32_t (*wred)[4], int* wtot) {
+    const float* p = sd.data + base;
+    WTP_CPROBE(0);
+    uint32_t kl, kh, sh;
+    float4 v[IT];
+    if constexpr (WIN) {
+        /* sample loads first, then the stream loads: the window is built while the chunk arrives */
+        uint32_t ks[M_SAMPLE / CT];
+        sample_keys<CT, M_SAMPLE>(sd, ks);
+        if (FULL) load_chunk<IT, CT>(p, v);
+        else load_chunk_ragged<IT, CT>(p, len, v);
+        window_from_keys<CT, M_SAMPLE>(sd, ks, *wl, &kl, &kh, &sh);
+        if (first && threadIdx.x == 0) { st->kl = kl; st->kh = kh; st->shift = sh; } /* for the select */
+    } else {
+        /* the window came from k_window; the stream loads go out first (the window words are
+         * scalar loads, counted separately from the vector loads) */
+        if (FULL) load_chunk<IT, CT>(p, v);
+        else load_chunk_ragged<IT, CT>(p, len, v);
+        kl = st->kl;
+        kh = st->kh;
+        sh = st->shift;
+    }
+    WTP_CPROBE(1);
+    uint32_t below, eql, mx, cnt;
+    collect_count<CT, IT>(v, FULL, len, 1 << sd.nsub_log2, kl, kh, lsub, stage, below, eql, mx, cnt);
+    collect_finish<CT>(sd, st, cand, kl, sh, below, eql, mx, cnt, lsub, lbase, stage, wred, wtot);
 }
 
 /* ------------------------------------------------------------- the select --- */
@@ -1216,7 +1242,7 @@ __device__ __forceinline__ bool res_wait(uint32_t* ctr, uint32_t want, uint64_t 
             const uint32_t v = ldc<true>(ctr);
             if (v & RES_POISON) break;
             if (v >= want) { ok = 1; break; }
-            if (wall_ticks() - t0 > timeout) {
+            if (wall_ticks() - t0 >= timeout) { /* >=: a zero bound poisons at the first incomplete look */
                 if (atomicCAS(ctr, v, v | RES_POISON) == v) break;
                 continue; /* it moved: look again */
             }
@@ -1521,7 +1547,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 const uint32_t x = ldc<true>(b1);
                 if (x & RES_POISON) break;
                 if (x >= nwg) { ok = 1; break; }
-                if (wall_ticks() - t0 > tmo) {
+                if (wall_ticks() - t0 >= tmo) {
                     if (atomicCAS(b1, x, x | RES_POISON) == x) break;
                     continue; /* it moved: look again */
                 }

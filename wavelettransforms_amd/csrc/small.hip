@@ -95,7 +95,7 @@ __device__ __forceinline__ bool sm_wait(uint32_t* ctr, uint32_t v0, uint32_t wan
         while (true) {
             if (v & RES_POISON) break;
             if (v >= want) { ok = 1; break; }
-            if (sm_ticks() - t0 > timeout) {
+            if (sm_ticks() - t0 >= timeout) { /* >=: a zero bound poisons at the first incomplete look */
                 const uint32_t w = atomicCAS(ctr, v, v | RES_POISON);
                 if (w == v) break;
                 v = w; /* it moved: look again */
