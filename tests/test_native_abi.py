@@ -104,6 +104,19 @@ def test_mode_switches_validate_and_return_the_previous_mode():
         setter(prev)
 
 
+def test_interior_mode_clamps_and_returns_the_previous_mode():
+    """wtp_set_interior: 0 / 1 / 2, values outside clamped, the previous mode returned (host logic
+    only: the mode is read at the next filter-bank launch)."""
+    L = N.lib()
+    prev = L.wtp_set_interior(2)
+    assert prev in (0, 1, 2)
+    assert L.wtp_set_interior(0) == 2
+    assert L.wtp_set_interior(1) == 0
+    assert L.wtp_set_interior(7) == 1
+    assert L.wtp_set_interior(-3) == 2
+    assert L.wtp_set_interior(prev) == 0
+
+
 def test_integration_stub_is_the_documented_block():
     """INTEGRATION.md section 2's code block is exactly tests/integration_stub.py's body (the GPU
     suite runs that file: tests/test_gpu_integration_stub.py)."""

@@ -302,7 +302,7 @@ struct InvItem { /* one image batch's synthesis level k -> y (B, outH, outW) */
 };
 void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s);
 void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s);
-int fb_set_interior(int mode); /* interior filter-bank kernels on (1, default) / off; returns the previous */
+int fb_set_interior(int mode); /* filter-bank kernel choice 0..2 (wtp_set_interior); returns the previous */
 void launch_fwd_level(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* anext, float* P,
                       int64_t PR, int64_t PC, int64_t offR, int64_t offC, int last, hipStream_t s);
 void launch_inv_level(const float* a_src, int64_t a_bs, int64_t lda, int a_from_P, const float* P, int64_t PR,
