@@ -571,7 +571,26 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
     const float* x = g.in[item] + (int64_t)b * a.in_bs;
     WTP_FPROBE(0);
     /* 1. the input tile; every load of a thread in flight before its first LDS write */
-    if constexpr (EDGE) {
+    if (EDGE && a.al16 && !(a.R & 1) && a.R >= NRc && a.C >= TP) {
+        /* a frame tile of an even, aligned level: the interior kernel's float4 rows, each row and
+         * each float4 wrapped once (C % 4 == 0 and the tile's first column is 16-byte aligned, so
+         * a float4 lies wholly inside or wholly across the edge; periodic, no repeat-last) */
+        constexpr int NE = NRc * W4, K = (NE + FB_THREADS - 1) / FB_THREADS;
+        const int start = gc0 - S0;
+        float4 q[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int e = min(k * FB_THREADS + (int)threadIdx.x, NE - 1);
+            const int rr = e / W4, j4 = e - rr * W4;
+            int r = gr0 + rr, c = start + 4 * j4;
+            r = r < 0 ? r + a.R : (r >= a.R ? r - a.R : r);
+            c = c < 0 ? c + a.C : (c >= a.C ? c - a.C : c);
+            q[k] = *reinterpret_cast<const float4*>(x + (int64_t)r * a.C + c);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            reinterpret_cast<float4*>(T)[min(k * FB_THREADS + (int)threadIdx.x, NE - 1)] = q[k];
+    } else if constexpr (EDGE) {
         /* rows by wave (row index and extension are scalar work), columns by lane; clamped
          * duplicates rewrite their own value */
         constexpr int RW = (NRc + 3) / 4, CW = (NCc + 63) / 64;
