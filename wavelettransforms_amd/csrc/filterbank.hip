@@ -613,15 +613,19 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
 #pragma unroll
             for (int c = 0; c < CW; ++c) T[min(wv + 4 * k, NRc - 1) * TP + S0 + min(lane + 64 * c, NCc - 1)] = v[k][c];
     } else {
-        /* whole float4 rows from the aligned column gc0 - S0 */
+        /* whole float4 rows from the aligned column gc0 - S0: buffer loads over the tile's rows, a
+         * 32-bit offset each (fwd_interior bounds the tile's span below 2^31 bytes) */
         constexpr int NE = NRc * W4, K = (NE + FB_THREADS - 1) / FB_THREADS;
-        const float* x0 = x + (int64_t)gr0 * a.C + (gc0 - S0);
+        const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(x) + (int64_t)gr0 * a.C + (gc0 - S0), 0, 4 * ((NRc - 1) * a.C + TP), 0x00020000);
         float4 q[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int e = min(k * FB_THREADS + (int)threadIdx.x, NE - 1);
             const int rr = e / W4, j4 = e - rr * W4;
-            q[k] = *reinterpret_cast<const float4*>(x0 + (int64_t)rr * a.C + 4 * j4);
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            const u4 w = __builtin_amdgcn_raw_buffer_load_b128(rX, 4 * (rr * a.C + 4 * j4), 0, 0);
+            q[k] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
         }
 #pragma unroll
         for (int k = 0; k < K; ++k)
@@ -1394,6 +1398,7 @@ static void fwd_int_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t 
  * offsets) -- k_fwd_level takes the whole grid. */
 static bool fwd_interior(const FwdArgs& a, int F, int* r0, int* nr, int* c0, int* nc) {
     if (!a.al16 || (int64_t)4 * a.P_bs > INT32_MAX || (int64_t)4 * a.Ro * a.Co > INT32_MAX) return false;
+    if ((int64_t)4 * (2 * FR + F) * a.C > INT32_MAX) return false; /* k_fwd_int's tile loads: 32-bit offsets */
     const int S0 = ((1 - F / 2) % 4 + 4) % 4, TP = (S0 + 2 * FC + F - 2 + 3) / 4 * 4, NR = 2 * FR + F - 2;
     int rlo = -1, rhi = -2, clo = -1, chi = -2;
     for (int tr = 0; tr < a.tilesR; ++tr) {
