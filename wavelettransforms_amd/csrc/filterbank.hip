@@ -276,9 +276,28 @@ struct FwdArgs {
  * a block's item is its tile / tiles-per-item.  The specialised kernels take their taps as a
  * SmallTaps (F <= 20): the whole argument stays near 2 KB. */
 constexpr int FB_UNI = 64;
+/* division by a launch-invariant d on the scalar unit (Granlund-Montgomery, exact for every 32-bit
+ * n): the tile decode's quotients are uniform, and the compiler's own division expands to a
+ * float reciprocal sequence on the VALU of every wave */
+struct FastDiv {
+    uint32_t m, sh; /* sh: first shift (0 or 1) | second shift << 8 */
+};
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+    const uint32_t u = (uint32_t)n, t = __umulhi(u, f.m);
+    return (int)((t + ((u - t) >> (f.sh & 0xFFu))) >> (f.sh >> 8));
+}
+static inline FastDiv make_fastdiv(uint32_t d) {
+    int l = 0;
+    while (l < 32 && (1ull << l) < d) ++l;
+    FastDiv f;
+    f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+    f.sh = l ? (1u | ((uint32_t)(l - 1) << 8)) : 0u;
+    return f;
+}
 struct FwdGroup {
     FwdArgs geo;            /* the items' geometry; its pointers are unused */
     int n, tiles;           /* items; tiles per item */
+    FastDiv dv_tiles, dv_per, dv_ntc; /* k_*_int: by tiles, by the rectangle's (or frame's) tiles, by nTC */
     const float* in[FB_UNI];
     float* anext[FB_UNI];
     float* P[FB_UNI];
@@ -550,18 +569,18 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
     float* T = lds;
     float2* LH = reinterpret_cast<float2*>(lds);
     const int gt = xcd_tile(blockIdx.x, gridDim.x);
-    const int item = gt / g.tiles;
+    const int item = fdiv(gt, g.dv_tiles);
     const FwdArgs& a = g.geo;
     const int tile = gt - item * g.tiles;
     int b, trow, tcol;
     if constexpr (EDGE) {
         const int per = a.tilesR * a.tilesC - a.nTR * a.nTC;
-        b = tile / per;
+        b = fdiv(tile, g.dv_per);
         frame_tile(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, &trow, &tcol);
     } else {
         const int per = a.nTR * a.nTC;
-        b = tile / per;
-        const int t2 = tile - b * per, trr = t2 / a.nTC;
+        b = fdiv(tile, g.dv_per);
+        const int t2 = tile - b * per, trr = fdiv(t2, g.dv_ntc);
         trow = a.tr0 + trr;
         tcol = a.tc0 + t2 - trr * a.nTC;
     }
@@ -778,14 +797,18 @@ struct InvArgs {
 /* the inverse's items of one geometry: per item its approximation source, packed array and output,
  * and its threshold / zero-count words as element offsets from the geometry's thr / zc (every
  * tensor of a call has them in one array) */
+__host__ __device__ inline int thr_off_of(int32_t v) { return (int)(int16_t)(v & 0xFFFF); }
+__host__ __device__ inline int zc_off_of(int32_t v) { return (int)(v >> 16); }
 struct InvGroup {
     InvArgs geo;
     int n, tiles;
+    FastDiv dv_tiles, dv_per, dv_ntc; /* as FwdGroup */
     const float* a[FB_UNI];
     const float* P[FB_UNI];
     float* y[FB_UNI];
-    int32_t thr_off[FB_UNI]; /* 32-bit: a scalar load (a 16-bit kernarg element is a vector load and a wait) */
-    int32_t zc_off[FB_UNI];
+    /* threshold (low 16 bits) and zero-count (high 16 bits) word offsets, signed, packed in one
+     * 32-bit element: a scalar load (a 16-bit kernarg element is a vector load and a wait) */
+    int32_t tz_off[FB_UNI];
 };
 
 template <int FT>
@@ -799,8 +822,8 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
     a.a = g.a[item];
     a.P = g.P[item];
     a.y = g.y[item];
-    a.thr = a.thr ? a.thr + g.thr_off[item] : nullptr;
-    a.zc = a.zc ? a.zc + g.zc_off[item] : nullptr;
+    a.thr = a.thr ? a.thr + thr_off_of(g.tz_off[item]) : nullptr;
+    a.zc = a.zc ? a.zc + zc_off_of(g.tz_off[item]) : nullptr;
     const int tile = gt - item * g.tiles;
     int tc, tr, b;
     if (a.frame) {
@@ -1093,18 +1116,18 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
     constexpr int H = FT / 2, HM = H;
     constexpr int NR = IR / 2 + H - (H & 1), NC = IC / 2 + H - (H & 1); /* coefficient rows / columns */
     const int gt = xcd_tile(blockIdx.x, gridDim.x);
-    const int item = gt / g.tiles;
+    const int item = fdiv(gt, g.dv_tiles);
     const InvArgs& a = g.geo;
     const int tile = gt - item * g.tiles;
     int b, trow, tcol;
     if constexpr (EDGE) {
         const int per = a.tilesR * a.tilesC - a.nTR * a.nTC;
-        b = tile / per;
+        b = fdiv(tile, g.dv_per);
         frame_tile(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, &trow, &tcol);
     } else {
         const int per = a.nTR * a.nTC;
-        b = tile / per;
-        const int t2 = tile - b * per, trr = t2 / a.nTC;
+        b = fdiv(tile, g.dv_per);
+        const int t2 = tile - b * per, trr = fdiv(t2, g.dv_ntc);
         trow = a.tr0 + trr;
         tcol = a.tc0 + t2 - trr * a.nTC;
     }
@@ -1114,7 +1137,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
     float2* Aq = reinterpret_cast<float2*>(lds); /* (cA, cH=da) */
     float2* Dq = Aq + NR * NC;                   /* (cV=ad, cD=dd) */
     float2* LoHi = Aq;                           /* NR x IC, written over Aq/Dq after the row pass */
-    const float* thrp = a.thr ? a.thr + g.thr_off[item] : nullptr;
+    const float* thrp = a.thr ? a.thr + thr_off_of(g.tz_off[item]) : nullptr;
     const float thr = thrp ? *thrp : 0.0f; /* |c| < 0 never holds: no threshold */
     auto tl = [&](float c) { return (fabsf(c) < thr) ? 0.0f : c; };
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1337,7 +1360,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
         __syncthreads();
         if (lane == 0 && z) atomicAdd(&zs, (unsigned long long)z);
         __syncthreads();
-        if (threadIdx.x == 0 && zs) atomicAdd(a.zc + g.zc_off[item], zs);
+        if (threadIdx.x == 0 && zs) atomicAdd(a.zc + zc_off_of(g.tz_off[item]), zs);
     }
     WTP_FPROBE(3);
 }
@@ -1626,11 +1649,16 @@ void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) 
             g.geo.tr0 = r0; g.geo.nTR = nr; g.geo.tc0 = c0; g.geo.nTC = nc;
             FwdGroup gi = g;
             gi.tiles = nr * nc * B;
+            gi.dv_tiles = make_fastdiv((uint32_t)gi.tiles);
+            gi.dv_per = make_fastdiv((uint32_t)(nr * nc));
+            gi.dv_ntc = make_fastdiv((uint32_t)nc);
             const int fr = g.geo.tilesR * g.geo.tilesC - nr * nc;
             fwd_interior_go<false>(gi, gi.n * gi.tiles, tp, s);
             if (fr == 0) continue;
             g.geo.frame = 1;
             g.tiles = fr * B;
+            g.dv_tiles = make_fastdiv((uint32_t)g.tiles);
+            g.dv_per = make_fastdiv((uint32_t)fr);
             if (mode == 2) {
                 fwd_interior_go<true>(g, g.n * g.tiles, tp, s);
                 continue;
@@ -1672,8 +1700,8 @@ void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s) 
             g.a[m] = x.a;
             g.P[m] = x.P;
             g.y[m] = x.y;
-            g.thr_off[m] = x.thr ? (int32_t)(x.thr - g.geo.thr) : 0;
-            g.zc_off[m] = x.zc ? (int32_t)(x.zc - g.geo.zc) : 0;
+            const int32_t to = x.thr ? (int32_t)(x.thr - g.geo.thr) : 0, zo = x.zc ? (int32_t)(x.zc - g.geo.zc) : 0;
+            g.tz_off[m] = (int32_t)(((uint32_t)zo << 16) | ((uint32_t)to & 0xFFFFu)); /* off_ok: both within int16 */
         }
         int r0, nr, c0, nc;
         const int mode = g_fb_interior.load(std::memory_order_relaxed);
@@ -1683,11 +1711,16 @@ void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s) 
             g.geo.tr0 = r0; g.geo.nTR = nr; g.geo.tc0 = c0; g.geo.nTC = nc;
             InvGroup gi = g;
             gi.tiles = nr * nc * B;
+            gi.dv_tiles = make_fastdiv((uint32_t)gi.tiles);
+            gi.dv_per = make_fastdiv((uint32_t)(nr * nc));
+            gi.dv_ntc = make_fastdiv((uint32_t)nc);
             const int fr = g.geo.tilesR * g.geo.tilesC - nr * nc;
             inv_interior_go<false>(gi, gi.n * gi.tiles, tp, s);
             if (fr == 0) continue;
             g.geo.frame = 1;
             g.tiles = fr * B;
+            g.dv_tiles = make_fastdiv((uint32_t)g.tiles);
+            g.dv_per = make_fastdiv((uint32_t)fr);
             if (mode == 2 && inv_frame_ok(g.geo, tp.F)) {
                 inv_interior_go<true>(g, g.n * g.tiles, tp, s);
                 continue;
