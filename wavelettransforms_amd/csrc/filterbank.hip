@@ -298,6 +298,7 @@ struct FwdGroup {
     FwdArgs geo;            /* the items' geometry; its pointers are unused */
     int n, tiles;           /* items; tiles per item */
     FastDiv dv_tiles, dv_per, dv_ntc; /* k_*_int: by tiles, by the rectangle's (or frame's) tiles, by nTC */
+    FastDiv dv_tc, dv_side;           /* the frame's decode: by tilesC, by tilesC - nTC */
     const float* in[FB_UNI];
     float* anext[FB_UNI];
     float* P[FB_UNI];
@@ -324,6 +325,28 @@ __device__ __forceinline__ void frame_tile(int f, int tilesC, int r0, int nr, in
     f -= nr * side;
     *tr = r0 + nr + f / tilesC;
     *tc = f - (f / tilesC) * tilesC;
+}
+
+/* frame_tile with the divisions by tilesC and tilesC - nc on the scalar unit */
+__device__ __forceinline__ void frame_tile_fd(int f, int tilesC, int r0, int nr, int c0, int nc, const FastDiv& dtc,
+                                              const FastDiv& dside, int* tr, int* tc) {
+    const int top = r0 * tilesC, side = tilesC - nc;
+    if (f < top) {
+        *tr = fdiv(f, dtc);
+        *tc = f - *tr * tilesC;
+        return;
+    }
+    f -= top;
+    if (f < nr * side) {
+        const int q = fdiv(f, dside), k = f - q * side;
+        *tr = r0 + q;
+        *tc = k < c0 ? k : k + nc;
+        return;
+    }
+    f -= nr * side;
+    const int q = fdiv(f, dtc);
+    *tr = r0 + nr + q;
+    *tc = f - q * tilesC;
 }
 
 /* taps of the interior kernels: analysis {dec_lo[j], dec_hi[j]} adjacent, so one SGPR pair is
@@ -576,7 +599,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
     if constexpr (EDGE) {
         const int per = a.tilesR * a.tilesC - a.nTR * a.nTC;
         b = fdiv(tile, g.dv_per);
-        frame_tile(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, &trow, &tcol);
+        frame_tile_fd(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, g.dv_tc, g.dv_side, &trow, &tcol);
     } else {
         const int per = a.nTR * a.nTC;
         b = fdiv(tile, g.dv_per);
@@ -803,6 +826,7 @@ struct InvGroup {
     InvArgs geo;
     int n, tiles;
     FastDiv dv_tiles, dv_per, dv_ntc; /* as FwdGroup */
+    FastDiv dv_tc, dv_side;
     const float* a[FB_UNI];
     const float* P[FB_UNI];
     float* y[FB_UNI];
@@ -1123,7 +1147,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
     if constexpr (EDGE) {
         const int per = a.tilesR * a.tilesC - a.nTR * a.nTC;
         b = fdiv(tile, g.dv_per);
-        frame_tile(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, &trow, &tcol);
+        frame_tile_fd(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, g.dv_tc, g.dv_side, &trow, &tcol);
     } else {
         const int per = a.nTR * a.nTC;
         b = fdiv(tile, g.dv_per);
@@ -1659,6 +1683,8 @@ void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) 
             g.tiles = fr * B;
             g.dv_tiles = make_fastdiv((uint32_t)g.tiles);
             g.dv_per = make_fastdiv((uint32_t)fr);
+            g.dv_tc = make_fastdiv((uint32_t)g.geo.tilesC);
+            g.dv_side = make_fastdiv((uint32_t)std::max(1, g.geo.tilesC - nc));
             if (mode == 2) {
                 fwd_interior_go<true>(g, g.n * g.tiles, tp, s);
                 continue;
@@ -1721,6 +1747,8 @@ void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s) 
             g.tiles = fr * B;
             g.dv_tiles = make_fastdiv((uint32_t)g.tiles);
             g.dv_per = make_fastdiv((uint32_t)fr);
+            g.dv_tc = make_fastdiv((uint32_t)g.geo.tilesC);
+            g.dv_side = make_fastdiv((uint32_t)std::max(1, g.geo.tilesC - nc));
             if (mode == 2 && inv_frame_ok(g.geo, tp.F)) {
                 inv_interior_go<true>(g, g.n * g.tiles, tp, s);
                 continue;
