@@ -110,6 +110,9 @@ __device__ __forceinline__ bool sm_wait(uint32_t* ctr, uint32_t v0, uint32_t wan
     return *s_ok != 0;
 }
 
+/* two lanes of packed FP32 (v_pk_mul_f32 / v_pk_add_f32): the same IEEE operations per lane */
+typedef float sf2 __attribute__((ext_vector_type(2)));
+
 /* e / n and e % n for e < 2^24 without an integer division (n uniform, inv = 1.0f / n) */
 __device__ __forceinline__ void sm_divmod(int e, int n, float inv, int* q, int* r) {
     int d = (int)((float)e * inv);
@@ -412,11 +415,11 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                     float v[FT > 0 ? FT : 1];
 #pragma unroll
                     for (int qq = 0; qq < FT; ++qq) v[qq] = Xc[(s0 - qq) * pc.len + mc];
+                    sf2 ad2 = {0.0f, 0.0f}; /* (a, d) packed */
                     sm_order<FT>(c1, __all(c1 == 0), [&](int j) { return v[j]; }, [&](int j) { return j; },
-                                 [&](int j, float x) {
-                                     a = a + staps[0][j] * x;
-                                     d = d + staps[1][j] * x;
-                                 });
+                                 [&](int j, float x) { ad2 = ad2 + sf2{staps[0][j], staps[1][j]} * sf2{x, x}; });
+                    a = ad2.x;
+                    d = ad2.y;
                 } else {
                     const SmAna an = sm_ana_at(wr, Nr, Npr, F, mr);
                     for (int qq = 0; qq < F; ++qq) {
@@ -450,14 +453,18 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                     float2 v[FT > 0 ? FT : 1];
 #pragma unroll
                     for (int qq = 0; qq < FT; ++qq) v[qq] = row[s0 - qq];
+                    sf2 lo2 = {0.0f, 0.0f}, hi2 = {0.0f, 0.0f}; /* (aa, da), (ad, dd) packed */
                     sm_order<FT>(c1, __all(c1 == 0), [&](int j) { return v[j]; }, [&](int j) { return j; },
                                  [&](int j, float2 x) {
                                      const float c0 = staps[0][j], c1v = staps[1][j];
-                                     aa = aa + c0 * x.x;
-                                     ad = ad + c1v * x.x;
-                                     da = da + c0 * x.y;
-                                     dd = dd + c1v * x.y;
+                                     const sf2 xv = {x.x, x.y};
+                                     lo2 = lo2 + sf2{c0, c0} * xv;
+                                     hi2 = hi2 + sf2{c1v, c1v} * xv;
                                  });
+                    aa = lo2.x;
+                    da = lo2.y;
+                    ad = hi2.x;
+                    dd = hi2.y;
                 } else {
                     const SmAna an = sm_ana_at(wc, Nc, Npc, F, mc);
                     for (int qq = 0; qq < F; ++qq) {
@@ -838,18 +845,15 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
                         vh[qq] = tl(cH[b0 - qq]);
                         vd[qq] = tl(cD[b0 - qq]);
                     }
-                    sm_order<HT>(c1, plain, [&](int j) { return make_float2(va[j], vh[j]); },
+                    sf2 lh = {0.0f, 0.0f}; /* (lo, hi) packed */
+                    sm_order<HT>(c1, plain, [&](int j) { return sf2{va[j], vh[j]}; },
                                  [&](int j) { return staps[2][2 * j + par]; },
-                                 [&](float cf, float2 x) {
-                                     lo = lo + cf * x.x;
-                                     hi = hi + cf * x.y;
-                                 });
-                    sm_order<HT>(c1, plain, [&](int j) { return make_float2(vv[j], vd[j]); },
+                                 [&](float cf, sf2 x) { lh = lh + sf2{cf, cf} * x; });
+                    sm_order<HT>(c1, plain, [&](int j) { return sf2{vv[j], vd[j]}; },
                                  [&](int j) { return staps[3][2 * j + par]; },
-                                 [&](float cf, float2 x) {
-                                     lo = lo + cf * x.x;
-                                     hi = hi + cf * x.y;
-                                 });
+                                 [&](float cf, sf2 x) { lh = lh + sf2{cf, cf} * x; });
+                    lo = lh.x;
+                    hi = lh.y;
                 } else {
                     const SmSyn sy = sm_syn_at(oc, Noc, Nc, F, mc);
                     for (int qq = 0; qq < HH; ++qq) {
