@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build libwtprune.so from a git revision (default HEAD) into tools/ab/libwtprune_base.so, for
-# same-box A/B runs against the working tree (tools/gpu_resab.sh).  tools/ab/ travels to the GPU
+# same-box A/B runs against the working tree (tools/gpu_ab.sh).  tools/ab/ travels to the GPU
 # box (.so files are git-ignored, not gpurun-ignored).
 set -e
 REV=${1:-HEAD}

@@ -1,26 +1,32 @@
 #!/bin/bash
-# A/B of k_resident variants (env knobs read by launch_resident): resident parity tests under
-# each variant, then the cfg2 bench per variant (ms/step and the k_resident stage time).
-# Usage: gpurun --timeout 900 -- bash tools/gpu_ab.sh TAG "OPTS:SIGMA" ["OPTS:SIGMA" ...]
+# A/B on one box: parity of the changed paths, then each config's bench line with the
+# working tree's library ("new") and tools/ab/libwtprune_base.so ("base", tools/build_base.sh),
+# alternated twice; the k_resident phase lab last.
+# Usage: gpurun --timeout 1100 -- bash tools/gpu_ab.sh TAG [configs]
 set -o pipefail
-TAG=$1; shift
-ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$ROOT"
-OUT=$ROOT/gpurun_out
-mkdir -p "$OUT"
+TAG=${1:-ab}
+CFGS=${2:-"cfg2 cfg3 cfg5"}
+cd ${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=gpurun_out
+mkdir -p $OUT
 export TMPDIR=/tmp
-for v in "$@"; do
-  export WTP_RES_OPTS=${v%%:*} WTP_RES_SIGMA=${v##*:}
-  timeout -k 10 300 python -u -m pytest tests/test_gpu_resident.py -x -q --timeout 120 --timeout-method thread \
-      > "$OUT/ab_${TAG}_$v.log" 2>&1 || { echo "tests failed for $v"; tail -40 "$OUT/ab_${TAG}_$v.log"; exit 1; }
-  echo "$v tests: $(tail -1 "$OUT/ab_${TAG}_$v.log")"
-done
-for rep in 1 2; do
-  for v in "$@"; do
-    export WTP_RES_OPTS=${v%%:*} WTP_RES_SIGMA=${v##*:}
-    timeout -k 10 300 python bench.py --no-cpu --steps 1000 > "$OUT/abb_${TAG}_$v.log" 2>&1 || { echo "bench failed for $v"; tail -20 "$OUT/abb_${TAG}_$v.log"; exit 1; }
+echo "== parity"
+timeout -k 10 700 python -u -m pytest tests/test_gpu_resident.py tests/test_gpu_small.py tests/test_gpu_large_levels.py tests/test_gpu_parity.py tests/test_gpu_pipeline.py tests/test_gpu_cfg5_bench_call.py -x -q --timeout 300 --timeout-method thread > $OUT/par_$TAG.log 2>&1 || { echo parity failed; grep -E "FAIL|Error|assert" $OUT/par_$TAG.log | head -30; tail -30 $OUT/par_$TAG.log; exit 1; }
+tail -1 $OUT/par_$TAG.log
+for c in $CFGS; do
+  X=""; [ $c = cfg5 ] && X="--steps 10 --warmup 2 --replays 10"
+  for v in new base new base; do
+    L=""; [ $v = base ] && L=$(pwd)/tools/ab/libwtprune_base.so
+    WTP_LIB_PATH=$L timeout -k 10 300 python bench.py --config $c --no-cpu --no-cold $X > $OUT/b_${TAG}_${c}_$v.log 2>&1 || { tail -20 $OUT/b_${TAG}_${c}_$v.log; exit 1; }
     python3 -c "
-import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print(sys.argv[2], 'ms/step %.5f'%d['ms_per_step'], 'stage', {k: round(v,2) for k,v in d['stage_us'].items()})" "$OUT/abb_${TAG}_$v.log" "$v"
+import json
+d=json.loads([l for l in open('$OUT/b_${TAG}_${c}_$v.log') if l.startswith('{')][-1]); r=d['roofline']
+print('$c', '$v', round(d['ms_per_step']*1e3,2), 'us/step', r.get('kernel'), round(r.get('avg_launch_us') or -1,2), 'frac', round(r.get('frac') or -1,3))"
   done
 done
+if [ -n "$RESLAB" ]; then
+  echo "== reslab"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/mb/reslab.hip -o /tmp/reslab || exit 1
+  timeout -k 10 120 /tmp/reslab 50 $OUT/reslab_$TAG.csv > $OUT/reslab_$TAG.log 2>&1 || { echo reslab failed; tail -20 $OUT/reslab_$TAG.log; exit 1; }
+  grep -v "184466" $OUT/reslab_$TAG.log | head -30
+fi
