@@ -75,6 +75,10 @@ def parse():
                     help="run every filter-bank tile in the general kernel (wtp_set_interior(0); A/B only)")
     ap.add_argument("--frame-general", action="store_true",
                     help="run the frame of edge tiles in the general kernel (wtp_set_interior(1); A/B only)")
+    ap.add_argument("--pipeline", type=int, default=None,
+                    help="wtp_set_pipeline mode for multi-group calls (default: the library's; A/B only)")
+    ap.add_argument("--frame-apart", action="store_true",
+                    help="the frame of edge tiles in a launch of its own (wtp_set_interior(2); A/B only)")
     ap.add_argument("--no-rocprof", action="store_true", help="skip the in-run rocprofv3 kernel-stats child")
     ap.add_argument("--profile-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
@@ -134,6 +138,10 @@ def rocprof_child(args, timeout=240):
         cmd.append("--no-interior")
     if args.frame_general:
         cmd.append("--frame-general")
+    if args.frame_apart:
+        cmd.append("--frame-apart")
+    if args.pipeline is not None:
+        cmd += ["--pipeline", str(args.pipeline)]
     env = dict(os.environ, TMPDIR="/tmp")
     try:
         subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
@@ -260,6 +268,10 @@ def main():
         engine.set_interior(False)
     elif args.frame_general:
         engine.set_interior(1)
+    elif args.frame_apart:
+        engine.set_interior(2)
+    if args.pipeline is not None:
+        engine.set_pipeline(args.pipeline)
 
     # ---------------------------------------------------------------- workload
     if args.config == "cfg2":

@@ -184,14 +184,17 @@ unsigned wtp_set_resident_timeout_us(unsigned us);
  * group's percentile selection on a side stream of the library's (one per device and caller
  * stream, non-blocking, created on first use), overlapping the next group's forward transform;
  * the caller's stream waits for it before that group's inverse, so the call stays ordered on
- * the caller's stream (graph capture included).  Mode 0: everything on the caller's stream.
- * Returns the previous mode (process-wide). */
+ * the caller's stream (graph capture included).  Mode 2: every group's forward and inverse on a
+ * lane stream of its own (group g + 1's forward starts once group g's first two levels are done),
+ * the selections on the side stream, every lane and the side stream joined back into the
+ * caller's stream at the end of the call.  Mode 0: everything on the caller's stream.  Returns
+ * the previous mode (process-wide). */
 int wtp_set_pipeline(int mode);
 /* The filter-bank levels run their interior tiles (input window inside the image, full tile)
- * in kernels compiled without the edge forms.  Mode 2 (default): the frame of edge tiles in the
- * same kernels' edge-capable form; mode 1: the frame in the general kernel; mode 0: every tile in
- * the general kernel (identical results in every mode).  Returns the previous mode
- * (process-wide). */
+ * in kernels compiled without the edge forms.  Mode 3 (default): the frame of edge tiles in the
+ * same kernels' edge-capable form, in the same launch as the interior; mode 2: the same as two
+ * launches; mode 1: the frame in the general kernel; mode 0: every tile in the general kernel
+ * (identical results in every mode).  Returns the previous mode (process-wide). */
 int wtp_set_interior(int mode);
 #define WTP_PATH_SMALL 4 /* every tensor of the call ran in one launch (2-D transforms, small population) */
 /* measurement hook (bench.py): while set, every resident launch atomically lowers stamps_dev[0] to

@@ -47,25 +47,26 @@ def test_large_levels_equal_oracle(wavelet):
 @pytest.mark.parametrize("wavelet", WAVELETS)
 def test_interior_kernels_equal_general(wavelet):
     """The interior filter-bank kernels (k_fwd_int / k_inv_int) with the frame of edge tiles in
-    their EDGE form (mode 2, the default) and in the general kernels (mode 1), against every tile
+    their EDGE form, in the interior's launch (mode 3, the default) or in a launch of its own (mode
+    2), and in the general kernels (mode 1), against every tile
     in the general kernels (mode 0): packed coefficients and pruned outputs bit for bit, on shapes
     with an interior and a frame (odd extents, batches, partial last tiles, a 2-level and a 4-level
     tree; the deepest levels of the narrow shape fall back to the general frame)."""
     shapes = [(1, 2, 700, 1100), (1, 1, 1031, 515), (800, 1600), (2, 1, 333, 4100)]
-    prev = eng.set_interior(2)
+    prev = eng.set_interior(3)
     try:
         for j, shp in enumerate(shapes):
             e = G.W.sigma_exponent((2.0 / (shp[-1] * shp[-2])) ** 0.5)
             x = eng.synth(shp, 41, j, e)
             for level in (2, 4):
                 res = []
-                for mode in (2, 1, 0):
+                for mode in (3, 2, 1, 0):
                     eng.set_interior(mode)
                     P = eng.wavedec2_packed(x, wavelet, level).cpu().numpy().view(np.uint32)
                     outs, (r,) = eng.prune([x], wavelet, level, 61.8)
                     res.append((P, outs[0].cpu().numpy().view(np.uint32), r["zero_count"], r["thr64"]))
                 Pg, og, zg, tg = res[-1]
-                for m, (Pm, om, zm, tm) in zip((2, 1), res[:2]):
+                for m, (Pm, om, zm, tm) in zip((3, 2, 1), res[:3]):
                     assert np.array_equal(Pm, Pg), (shp, level, m)
                     assert np.array_equal(om, og), (shp, level, m)
                     assert zm == zg and G.f64_bits_equal(tm, tg), (shp, level, m)

@@ -1,9 +1,11 @@
 """GPU parity of the pipelined form of a multi-group call (include/wtprune.h wtp_set_pipeline):
 with more than one launch group (24 tensors) of wavelet-transformed tensors, each group's
 selection runs on the library's side stream while the caller's stream runs the next group's
-forward levels.  The results must equal the single-stream form and the C oracle bit for bit
-(values, float64 threshold bits, zero counts), eagerly and inside a captured HIP graph, on the
-caller's default and non-default streams; a level-0 tensor mixed into a group is covered too."""
+forward levels (mode 1), or each group's forward and inverse run on a lane stream of its own,
+staggered by two levels, with the selections on the side stream (mode 2).  The results must equal
+the single-stream form and the C oracle bit for bit (values, float64 threshold bits, zero counts),
+eagerly and inside a captured HIP graph, on the caller's default and non-default streams; a
+level-0 tensor mixed into a group is covered too."""
 import numpy as np
 import pytest
 import torch
@@ -51,11 +53,12 @@ def _equal(a, b):
         assert G.f64_bits_equal(p["thr64"], q["thr64"])
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("wavelet,level,pct", [("db8", 3, 60.0), ("bior3.3", 5, 50.0), ("haar", 2, 0.0)])
-def test_pipelined_equals_single_stream_and_oracle(eng, wavelet, level, pct):
+def test_pipelined_equals_single_stream_and_oracle(eng, wavelet, level, pct, mode):
     xs = _inputs(eng)
-    a = _run(eng, xs, True, wavelet, level, pct)
-    b = _run(eng, xs, False, wavelet, level, pct)
+    a = _run(eng, xs, mode, wavelet, level, pct)
+    b = _run(eng, xs, 0, wavelet, level, pct)
     _equal(a, b)
     for i in (0, 1, 25, 48, 50):  # every group, the level-0 tensor, the odd shapes
         ref, rr = O.prune_tensor(G.W.synth_numpy(SHAPES[i], 7, i, 6 + (i % 5)), wavelet, level, pct)
@@ -64,19 +67,22 @@ def test_pipelined_equals_single_stream_and_oracle(eng, wavelet, level, pct):
         assert G.f64_bits_equal(a[1][i]["thr64"], rr["thr64"])
 
 
-def test_pipelined_on_a_side_stream_of_the_caller(eng):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_pipelined_on_a_side_stream_of_the_caller(eng, mode):
     xs = _inputs(eng)
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
-        a = _run(eng, xs, True, stream=s)
-    _equal(a, _run(eng, xs, False))
+        a = _run(eng, xs, mode, stream=s)
+    _equal(a, _run(eng, xs, 0))
 
 
-def test_pipelined_graph_capture_and_replay(eng):
-    """The side stream forks from and joins the captured stream: the graph replays the call."""
+@pytest.mark.parametrize("mode", [1, 2])
+def test_pipelined_graph_capture_and_replay(eng, mode):
+    """The side stream (and the lanes) fork from and join the captured stream: the graph replays
+    the call; several calls in one capture, as bench.py captures its steps."""
     xs = _inputs(eng)
-    ref = _run(eng, xs, False)
-    prev = eng.set_pipeline(True)
+    ref = _run(eng, xs, 0)
+    prev = eng.set_pipeline(mode)
     try:
         outs = [torch.empty_like(x) for x in xs]
         s = torch.cuda.Stream()
@@ -87,7 +93,8 @@ def test_pipelined_graph_capture_and_replay(eng):
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            _, resd = eng.launch(xs, "db8", 3, 60.0, outs=outs, carry_level=False)
+            for _ in range(3):
+                _, resd = eng.launch(xs, "db8", 3, 60.0, outs=outs, carry_level=False)
         for o in outs:
             o.zero_()
         g.replay()

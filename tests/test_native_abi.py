@@ -92,28 +92,30 @@ def test_workspace_size_covers_both_level_modes():
 
 
 def test_mode_switches_validate_and_return_the_previous_mode():
-    """wtp_set_resident / wtp_set_pipeline: 0 or 1, the previous mode returned, anything else
-    rejected with WTP_EARG and the mode left as it was (host logic only, no device work)."""
+    """wtp_set_resident (0 or 1) / wtp_set_pipeline (0, 1 or 2): the previous mode returned,
+    anything else rejected with WTP_EARG and the mode left as it was (host logic only, no device
+    work)."""
     L = N.lib()
-    for setter in (L.wtp_set_resident, L.wtp_set_pipeline):
+    for setter, top in ((L.wtp_set_resident, 1), (L.wtp_set_pipeline, 2)):
         prev = setter(0)
-        assert prev in (0, 1)
+        assert prev in range(top + 1)
         assert setter(1) == 0
-        assert setter(2) < 0 and setter(-1) < 0
-        assert setter(1) == 1  # unchanged by the rejected calls
+        assert setter(top + 1) < 0 and setter(-1) < 0
+        assert setter(top) == 1  # unchanged by the rejected calls
+        assert setter(1) == top
         setter(prev)
 
 
 def test_interior_mode_clamps_and_returns_the_previous_mode():
-    """wtp_set_interior: 0 / 1 / 2, values outside clamped, the previous mode returned (host logic
-    only: the mode is read at the next filter-bank launch)."""
+    """wtp_set_interior: 0 / 1 / 2 / 3, values outside clamped, the previous mode returned (host
+    logic only: the mode is read at the next filter-bank launch)."""
     L = N.lib()
     prev = L.wtp_set_interior(2)
-    assert prev in (0, 1, 2)
+    assert prev in (0, 1, 2, 3)
     assert L.wtp_set_interior(0) == 2
     assert L.wtp_set_interior(1) == 0
     assert L.wtp_set_interior(7) == 1
-    assert L.wtp_set_interior(-3) == 2
+    assert L.wtp_set_interior(-3) == 3
     assert L.wtp_set_interior(prev) == 0
 
 

@@ -11,7 +11,8 @@ OUT=gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
 echo "== parity"
-timeout -k 10 700 python -u -m pytest tests/test_gpu_resident.py tests/test_gpu_small.py tests/test_gpu_large_levels.py tests/test_gpu_parity.py tests/test_gpu_pipeline.py tests/test_gpu_cfg5_bench_call.py -x -q --timeout 300 --timeout-method thread > $OUT/par_$TAG.log 2>&1 || { echo parity failed; grep -E "FAIL|Error|assert" $OUT/par_$TAG.log | head -30; tail -30 $OUT/par_$TAG.log; exit 1; }
+PARITY=${PARITY:-tests/test_gpu_resident.py tests/test_gpu_small.py tests/test_gpu_large_levels.py tests/test_gpu_parity.py tests/test_gpu_pipeline.py tests/test_gpu_cfg5_bench_call.py}
+timeout -k 10 700 python -u -m pytest $PARITY -x -q --timeout 300 --timeout-method thread > $OUT/par_$TAG.log 2>&1 || { echo parity failed; grep -E "FAIL|Error|assert" $OUT/par_$TAG.log | head -30; tail -30 $OUT/par_$TAG.log; exit 1; }
 tail -1 $OUT/par_$TAG.log
 for c in $CFGS; do
   X=""; [ $c = cfg5 ] && X="--steps 10 --warmup 2 --replays 10"

@@ -46,10 +46,12 @@ __device__ bool poll_ge(const uint32_t* p, uint32_t want, uint32_t* err) {
     return ok;
 }
 
-/* the select chain: three dependent device reads, then the LDS select (a spin) */
-__device__ uint32_t chain(const uint32_t* tbl, uint32_t* lds) {
+/* the select chain: three dependent device reads of lines other CUs have just written (the
+ * segment's atomic bucket totals, then its workgroups' sc1 publications: 2 offsets each, then
+ * 264 keys), then the LDS select (a spin) */
+__device__ uint32_t chain(const uint32_t* tot, const uint32_t* pub, int b0, int nwg, uint32_t* lds) {
     const int tid = threadIdx.x, lane = tid & 63;
-    uint32_t a = ldc(tbl + 2 * tid) + ldc(tbl + 2 * tid + 1); /* 4 KB: the totals */
+    uint32_t a = ldc(tot + 2 * tid) + ldc(tot + 2 * tid + 1); /* 4 KB: the totals */
     lds[tid] = a;
     __syncthreads();
     uint32_t s = 0;
@@ -58,10 +60,13 @@ __device__ uint32_t chain(const uint32_t* tbl, uint32_t* lds) {
         s = __builtin_amdgcn_readfirstlane(s) & 0x10000u; /* 0 in practice, but a dependence */
     }
     __syncthreads();
-    if (tid < 64) lds[600 + lane] = ldc(tbl + 4096 + s + lane) + ldc(tbl + 4096 + s + 64 + lane); /* offsets */
+    if (tid < 64) {
+        const uint32_t* pw = pub + (int64_t)(b0 + lane % nwg) * 512;
+        lds[600 + lane] = ldc(pw + s + (lane & 7)) + ldc(pw + s + 8 + (lane & 7)); /* offsets */
+    }
     __syncthreads();
     const uint32_t o = lds[600] & 0x10000u;
-    uint32_t k = tid < 264 ? ldc(tbl + 8192 + o + tid) : 0u; /* the keys */
+    uint32_t k = tid < 264 ? ldc(pub + (int64_t)(b0 + tid % nwg) * 512 + o + tid / nwg) : 0u; /* the keys */
     lds[tid] = k;
     __syncthreads();
     if (tid == 0) {
@@ -69,7 +74,7 @@ __device__ uint32_t chain(const uint32_t* tbl, uint32_t* lds) {
         while (ticks() - t0 < 125) __builtin_amdgcn_s_sleep(1);
     }
     __syncthreads();
-    return lds[0];
+    return lds[0] & 0x10000u;
 }
 
 __global__ __launch_bounds__(CT) void k_sched(const float* __restrict__ x, float* __restrict__ y, Ws* ws,
@@ -87,11 +92,11 @@ __global__ __launch_bounds__(CT) void k_sched(const float* __restrict__ x, float
     const bool selector = b >= nchunks;
     if (selector) {
         /* selector of the multi-workgroup segment number (b - nchunks) */
-        int m = b - nchunks, s = 0;
-        for (; s < NSEG; ++s) if (c_wgs[s] > 1 && m-- == 0) break;
+        int m = b - nchunks, s = 0, sb = 0;
+        for (; s < NSEG; ++s) { if (c_wgs[s] > 1 && m-- == 0) break; sb += c_wgs[s]; }
         if (!(mode & REMOTE) || s >= NSEG) return;
         if (poll_ge(&ws->bar[s][0], epoch * c_wgs[s], &ws->err)) {
-            chain(tbl, lds);
+            chain(&ws->tot[s][0], pub, sb, c_wgs[s], lds);
             if (tid == 0) stc(&ws->flag[s][0], epoch);
         }
         if (tid == 0) atomicMax(stamps + 1, ticks());
@@ -146,7 +151,7 @@ __global__ __launch_bounds__(CT) void k_sched(const float* __restrict__ x, float
             if (mode & REMOTE) {
                 poll_ge(&ws->flag[seg][0], epoch, &ws->err);
             } else if (poll_ge(&ws->bar[seg][0], epoch * nwg, &ws->err)) {
-                mk += chain(tbl, lds);
+                mk += chain(&ws->tot[seg][0], pub, b0, nwg, lds);
             }
         } else {
             poll_ge(&ws->bar[seg][0], epoch * nwg, &ws->err);

@@ -1273,14 +1273,86 @@ __device__ __forceinline__ uint32_t parity_late(uint32_t qv) {
     return q;
 }
 
+/* The decided float4s of a chunk -- every key outside the window [kl, kh] -- stored before the
+ * threshold is known: a key below kl is below the threshold (kl <= ka <= thr32 when the window
+ * holds both ranks) and becomes +0.0, a key above kh stays.  Only out of place (the segment's
+ * input is intact for a full-scan fallback) and only as a first write: the last pass rewrites
+ * every float4 when the window missed or the threshold is NaN, else the pending ones (pend). */
+template <bool FULL>
+__device__ __forceinline__ void res_spec_store(const float4 (&v)[RES_IT], uint32_t pend, uint32_t kl, float* qo, int len,
+                                               bool al) {
+    constexpr int CT = RES_THREADS;
+    auto dec = [&](float xv) { return abs_key(xv) < kl ? 0.0f : xv; };
+    if (FULL) {
+        float4* q4 = reinterpret_cast<float4*>(qo);
+#pragma unroll
+        for (int it = 0; it < RES_IT; ++it) {
+            if ((pend >> it) & 1u) continue;
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v yv = {dec(v[it].x), dec(v[it].y), dec(v[it].z), dec(v[it].w)};
+            __builtin_nontemporal_store(yv, reinterpret_cast<f4v*>(q4 + it * CT + threadIdx.x));
+        }
+    } else {
+        const __amdgpu_buffer_rsrc_t rr = ragged_rsrc(qo, len);
+#pragma unroll
+        for (int it = 0; it < RES_IT; ++it) {
+            if ((pend >> it) & 1u) continue;
+            const float4 y = make_float4(dec(v[it].x), dec(v[it].y), dec(v[it].z), dec(v[it].w));
+            store4_tail(y, qo, rr, it * CT + (int)threadIdx.x, len, al);
+        }
+    }
+}
+
+/* k_resident's last pass: out = where(|x| < thr, 0, x) from registers for the float4s in fmask
+ * (every float4, or the pending ones where the decided ones went out ahead); a NaN threshold
+ * prunes nothing and the copy's zeros are counted (the pad slots read as +0.0 excluded) */
+template <bool FULL>
+__device__ __forceinline__ void res_final(const float4 (&v)[RES_IT], uint32_t pend, float thr, uint32_t fmask,
+                                          const SegDesc& sd, wtp_result* __restrict__ res, int64_t base, int len,
+                                          bool al) {
+    constexpr int CT = RES_THREADS, IT = RES_IT;
+    const int tid = threadIdx.x;
+    float* qo = sd.out + base;
+    auto fin = [&](float xv) { return (fabsf(xv) < thr) ? 0.0f : xv; };
+    if (FULL) {
+        float4* q4 = reinterpret_cast<float4*>(qo);
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            if (!((fmask >> it) & 1u)) continue;
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v yv = {fin(v[it].x), fin(v[it].y), fin(v[it].z), fin(v[it].w)};
+            __builtin_nontemporal_store(yv, reinterpret_cast<f4v*>(q4 + it * CT + tid));
+        }
+    } else {
+        const __amdgpu_buffer_rsrc_t rr = ragged_rsrc(qo, len);
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            if (!((fmask >> it) & 1u)) continue;
+            const float4 y = make_float4(fin(v[it].x), fin(v[it].y), fin(v[it].z), fin(v[it].w));
+            store4_tail(y, qo, rr, it * CT + tid, len, al);
+        }
+    }
+    if (thr != thr) { /* uniform */
+        uint32_t z = 0;
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) z += f4_get(v[it], c) == 0.0f;
+        const unsigned long long tot = block_sum_u64<CT>(z) - (unsigned long long)(RES_CHUNK - len);
+        if (tid == 0 && tot) atomicAdd((unsigned long long*)&res[sd.res].zero_count, tot);
+    }
+    WTP_RPROBE(7);
+}
+
 template <bool FULL>
 __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, SelHeader* __restrict__ head, uint32_t qv,
                                          uint32_t* __restrict__ cand, wtp_result* __restrict__ res,
                                          float* __restrict__ thr_out, int64_t base, int len, uint32_t* raw,
-                                         uint32_t* lsub, uint32_t (*wred)[8], uint32_t* wstage) {
+                                         uint32_t* lsub, uint32_t (*wred)[8], uint32_t* wstage, bool sel) {
     constexpr int CT = RES_THREADS, IT = RES_IT, NW = CT / 64;
     uint32_t q = 0;
-    const bool first = base == 0;
+    /* sel: this workgroup is its segment's selector (no chunk: len 0, its loads read nothing) */
+    const bool first = base == 0 && !sel;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const uint64_t tmo = t.res_timeout;
     WTP_RPROBE(0);
@@ -1390,6 +1462,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         sh = bits > RES_NSUB_LOG2 ? bits - RES_NSUB_LOG2 : 0;
     }
     uint32_t wbelow = 0, mx = 0, cnt = 0;
+    uint32_t pend = 0; /* bit it: float4 it holds a key inside [kl, kh] (its output waits for thr) */
     uint32_t* col = wstage + tid;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
@@ -1397,6 +1470,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
 #pragma unroll
         for (int c = 0; c < 4; ++c) k4[c] = abs_key(opaque(f4_get(v[it], c)));
         mx = max(mx, max(max(k4[0], k4[1]), max(k4[2], k4[3])));
+        uint32_t pin = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const uint32_t k = k4[c];
@@ -1404,8 +1478,12 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             wbelow += d >> 31;
             col[min(cnt, (uint32_t)RES_STG) * CT] = k;
             const bool valid = FULL || 4 * (it * CT + tid) + c < len;
-            cnt += (d <= span) & valid;
+            const uint32_t in = d <= span;
+            pin |= in;
+            cnt += in & valid;
         }
+        pend |= pin << it;
+        asm volatile("" : "+v"(pend)); /* kept as one word: left to itself the compiler keeps the 96 flags */
     }
     {
         wbelow = wave_sum_u32(wbelow);
@@ -1425,6 +1503,13 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
      * 1-3 us, and the solo segments were the launch's tail */
     const uint32_t nwg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
     const bool solo = nwg == 1u; /* block-uniform */
+    /* remote: a shared segment whose select runs on its selector workgroup (a CU that holds no
+     * chunk, so the select's dependent round trips queue behind nobody's stores); its workgroups
+     * only wait for the threshold granule, and out of place they store their decided float4s
+     * (res_spec_store) while the selector works */
+    const bool remote = t.nsel > 0 && !solo; /* block-uniform */
+    const bool spec = remote && !sel && sd.out != sd.data && !ovf;
+    const bool al = (sd.flags & SEG_ALIGNED) != 0;
     __shared__ unsigned long long s_cnt[1];
     __shared__ uint32_t s_mk, s_ovf;
     if (tid == 0) {
@@ -1436,7 +1521,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             s_cnt[0] = a0;
             s_mk = m2;
             s_ovf = ovf;
-        } else {
+        } else if (!sel) {
             const int sh8 = blockIdx.x & (NSHARD - 1);
             if (a0) atomicAdd(&st->below[sh8], a0);
             atomicMax(&st->maxkey[sh8], m2);
@@ -1457,7 +1542,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
                 if (j0 + u < cnt) atomicAdd(&lsub[(kk[u] - kl) >> sh], 1u);
         }
         __syncthreads();
-        if (!solo) {
+        if (!solo && !sel) {
 #pragma unroll
             for (int j = 0; j < BPT; ++j) { /* bucket j * CT + tid: 256 contiguous bytes per wave instruction */
                 const uint32_t c = lsub[j * CT + tid];
@@ -1471,7 +1556,10 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     uint32_t* b0 = reinterpret_cast<uint32_t*>(&st->seg_bar[0]);
     uint32_t* b1 = reinterpret_cast<uint32_t*>(&st->seg_bar[1]);
     uint32_t* b2 = reinterpret_cast<uint32_t*>(&st->seg_bar[2]);
-    if (!solo) res_arrive(b1);
+    if (!solo) {
+        if (sel) __syncthreads(); /* orders s_arr for wave 6 (the selector has no publication) */
+        else res_arrive(b1);
+    }
     WTP_RPROBE(4);
     /* ---- publication, while the segment gathers at barrier 1: this workgroup's inside keys,
      * bucket-sorted in LDS, and the bucket offsets (exclusive prefix of its bucket histogram),
@@ -1483,7 +1571,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     uint32_t* pos = raw;     /* bucket offsets (the window histogram is done with) */
     uint32_t* srt = wstage;  /* the sorted keys, over the columns */
     __shared__ uint32_t s_ok1;
-    if (!ovf) { /* block-uniform */
+    if (!ovf && !sel) { /* block-uniform */
         uint32_t kk[RES_STG];
 #pragma unroll
         for (int j = 0; j < RES_STG; ++j) kk[j] = col[j * CT]; /* entries past cnt are not used */
@@ -1538,8 +1626,13 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             if (s_arr == nsh - 1u && atomicAdd(&bar->arrive[0][16], 1u) == nact - 1u) stc(&head->parity, q + 1u);
         }
         if (tid == 0) s_ok1 = 1;
+    } else if (wv == NW - 1 && remote && !sel) {
+        /* a remote segment's workgroup does not wait at barrier 1: wave 7 stores its decided
+         * float4s at once (the others after their publication) */
+        if (lane == 0) s_ok1 = 1;
+        if (spec) res_spec_store<FULL>(v, pend, kl, sd.out + base, len, al);
     } else if (wv == NW - 1) {
-        /* ---- barrier 1, polled by wave 7 while the others store */
+        /* ---- barrier 1, polled by wave 7 while the others store (the selector: by wave 7) */
         if (lane == 0) {
             const uint64_t t0 = wall_ticks();
             uint32_t ok = 0;
@@ -1557,7 +1650,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         }
     } else {
         constexpr int ST = CT - 64; /* the storing threads */
-        if (!ovf) {
+        if (!ovf && !sel) {
             /* offsets: pub[b] = start of bucket b (pos[b - 1] now), pub[RES_NSUB] = the total */
             const __amdgpu_buffer_rsrc_t prs = region_rsrc(pub, RES_PUB_WORDS);
             if (tid < RES_NSUB / 4) {
@@ -1573,7 +1666,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         /* every storing wave drains; the last one to do so arrives at barrier 2 for the
          * workgroup (its LDS add follows every other storing wave's drain) */
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0 && atomicAdd(&s_pubn, 1u) == (uint32_t)(NW - 2)) atomicAdd(b2, 1u);
+        if (!sel && lane == 0 && atomicAdd(&s_pubn, 1u) == (uint32_t)(NW - 2)) atomicAdd(b2, 1u);
         /* the parity flip's second level: the last reader of a shard (blockIdx % 8) adds to the
          * top counter, whose last arrival flips the parity (every workgroup of the grid has read
          * it) -- wave 6, after its drain, off the barrier-1 poll */
@@ -1583,14 +1676,54 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);
             if (s_arr == nsh - 1u && atomicAdd(&bar->arrive[0][16], 1u) == nact - 1u) stc(&head->parity, q + 1u);
         }
+        if (spec) res_spec_store<FULL>(v, pend, kl, sd.out + base, len, al);
     }
     __syncthreads();
     WTP_RPROBE(11);
+    uint64_t* gr = reinterpret_cast<uint64_t*>(&st->thr_gr);
     if (!s_ok1) {
-        if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+        if (tid == 0) {
+            atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+            if (sel) atomicCAS(reinterpret_cast<unsigned long long*>(gr), 0ull, (unsigned long long)RES_GR_FAULT << 32);
+        }
         return; /* nothing stored to the output: the caller's input and output are untouched */
     }
     WTP_RPROBE(5);
+    if (remote && !sel) {
+        /* ---- the threshold granule {thr bits, tag} from the segment's selector (one 8-byte sc1
+         * word; the region is zero at the launch's start).  A wait that times out claims the
+         * granule for FAULT by compare-and-swap, so every workgroup of the segment and the
+         * selector agree: all store, or none does (in place: nothing was stored yet) */
+        __shared__ unsigned long long s_gr;
+        if (wv == NW - 1 && lane == 0) {
+            const uint64_t t0 = wall_ticks();
+            unsigned long long x;
+            while (true) {
+                x = ldc<true>(reinterpret_cast<const unsigned long long*>(gr));
+                if (x) break;
+                if (wall_ticks() - t0 >= tmo) {
+                    const unsigned long long f = (unsigned long long)RES_GR_FAULT << 32;
+                    const unsigned long long o = atomicCAS(reinterpret_cast<unsigned long long*>(gr), 0ull, f);
+                    x = o ? o : f;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_gr = x;
+        }
+        __syncthreads();
+        const unsigned long long g = s_gr;
+        const uint32_t tag = (uint32_t)(g >> 32);
+        if (tag & RES_GR_FAULT) {
+            if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+            return;
+        }
+        const float thr = __uint_as_float((uint32_t)g);
+        WTP_RPROBE(6);
+        res_final<FULL>(v, pend, thr, (spec && !(tag & RES_GR_ALL) && thr == thr) ? pend : 0xFFFFFFFFu, sd, res, base,
+                        len, al);
+        return;
+    }
     /* ---- P2: the segment's counters and bucket totals in one round trip (every load in
      * flight before any is used); a block scan of the totals names the bucket of each rank */
     __shared__ uint32_t s_wtot[NW], s_b2;
@@ -1698,7 +1831,10 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             WTP_PROBE(3);
             const uint32_t b2v = s_b2; /* block-uniform */
             if (!(b2v >= nwg && !(b2v & RES_POISON)) && !res_wait(b2, nwg, tmo)) {
-                if (tid == 0) atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+                if (tid == 0) {
+                    atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+                    if (sel) atomicCAS(reinterpret_cast<unsigned long long*>(gr), 0ull, (unsigned long long)RES_GR_FAULT << 32);
+                }
                 return;
             }
             WTP_PROBE(4);
@@ -1781,7 +1917,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     if (mk > 0x7F800000u) thr64 = __longlong_as_double(0x7FF8000000000000ll); /* NaN present: np.percentile is NaN */
     const float thr = (float)thr64;
     const bool nan = thr != thr; /* also inf - inf inside the lerp */
-    if (first) {
+    if (first || sel) {
         /* zeros of where(|x| < thr, 0, x) = #(key < tk), tk = bits(thr) when thr > 0, else 1 (only
          * the zeros themselves); ka <= thr <= kb and the ranks are adjacent, so #(key < tk) =
          * below + before + #(staged < tk).  A NaN threshold prunes nothing: every
@@ -1813,6 +1949,17 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             atomicMax(&r.path, path);
         }
     }
+    if (sel) {
+        /* the threshold granule for the segment's workgroups: {thr bits, tag}, claimed by
+         * compare-and-swap (a workgroup whose wait timed out may have claimed it for FAULT) */
+        if (tid == 0) {
+            const uint32_t tag = RES_GR_OK | (path == MODE_FULL ? RES_GR_ALL : 0u);
+            const unsigned long long gv = ((unsigned long long)tag << 32) | __float_as_uint(thr);
+            if (atomicCAS(reinterpret_cast<unsigned long long*>(gr), 0ull, gv) != 0ull)
+                atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+        }
+        return;
+    }
     if (path == MODE_FULL && sd.out == sd.data) { /* in place: nobody writes before the segment's scans end */
         res_arrive(b0);
         if (!res_wait(b0, nwg, tmo)) {
@@ -1822,37 +1969,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     }
     WTP_RPROBE(6);
     /* ---- P3: out = where(|x| < thr, 0, x) from registers (a NaN threshold prunes nothing) */
-    float* qo = sd.out + base;
-    auto fin = [&](float xv) { return (fabsf(xv) < thr) ? 0.0f : xv; };
-    if (FULL) {
-        float4* q4 = reinterpret_cast<float4*>(qo);
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            float4 y;
-            y.x = fin(v[it].x); y.y = fin(v[it].y); y.z = fin(v[it].z); y.w = fin(v[it].w);
-            typedef float f4v __attribute__((ext_vector_type(4)));
-            const f4v yv = {y.x, y.y, y.z, y.w};
-            __builtin_nontemporal_store(yv, reinterpret_cast<f4v*>(q4 + it * CT + tid));
-        }
-    } else {
-        const __amdgpu_buffer_rsrc_t rr = ragged_rsrc(qo, len);
-        const bool al = (sd.flags & SEG_ALIGNED) != 0;
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            float4 y;
-            y.x = fin(v[it].x); y.y = fin(v[it].y); y.z = fin(v[it].z); y.w = fin(v[it].w);
-            store4_tail(y, qo, rr, it * CT + tid, len, al);
-        }
-    }
-    if (nan) { /* uniform: the copy's zeros are counted (the pad slots read as +0.0 excluded) */
-        uint32_t z = 0;
-#pragma unroll
-        for (int it = 0; it < IT; ++it)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) z += f4_get(v[it], c) == 0.0f;
-        const unsigned long long tot = block_sum_u64<CT>(z) - (unsigned long long)(RES_CHUNK - len);
-        if (tid == 0 && tot) atomicAdd((unsigned long long*)&res[sd.res].zero_count, tot);
-    }
+    res_final<FULL>(v, pend, thr, 0xFFFFFFFFu, sd, res, base, len, al);
     WTP_RPROBE(7);
 }
 
@@ -1865,14 +1982,16 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(SegTable t, SelHeader*
     __shared__ __attribute__((aligned(16))) uint32_t wstage[(RES_STG + 1) * RES_THREADS]; /* 66 KB: RES_STG slots + the discard slot per thread */
     const uint32_t qv = ldc<true>(&head->parity); /* a vector load: see parity_late */
     if (t.stamps && threadIdx.x == 0) atomicMin(t.stamps, wall_ticks()); /* measurement only */
-    const int si = find_seg(t, blockIdx.x);
+    /* workgroups past the chunks are selectors, one per shared segment (t.sel_seg) */
+    const bool sel = (int)blockIdx.x >= t.nblk;
+    const int si = sel ? t.sel_seg[blockIdx.x - t.nblk] : find_seg(t, blockIdx.x);
     const SegDesc& sd = t.s[si];
-    const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * RES_CHUNK;
-    const int len = (int)min((int64_t)RES_CHUNK, sd.n - base);
+    const int64_t base = sel ? 0 : (int64_t)(blockIdx.x - sd.blk_begin) * RES_CHUNK;
+    const int len = sel ? 0 : (int)min((int64_t)RES_CHUNK, sd.n - base);
     if ((sd.flags & SEG_ALIGNED) && len == RES_CHUNK)
-        res_body<true>(t, sd, head, qv, cand, res, thr_out, base, len, raw, lsub, wred, wstage);
+        res_body<true>(t, sd, head, qv, cand, res, thr_out, base, len, raw, lsub, wred, wstage, false);
     else
-        res_body<false>(t, sd, head, qv, cand, res, thr_out, base, len, raw, lsub, wred, wstage);
+        res_body<false>(t, sd, head, qv, cand, res, thr_out, base, len, raw, lsub, wred, wstage, sel);
     if (t.stamps) { /* measurement only: the workgroup's end, once its stores have completed */
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -2340,7 +2459,15 @@ void launch_resident(const SegTable& t0, SelHeader* head, uint32_t* cand, wtp_re
     SegTable t = t0;
     t.res_timeout = g_res_timeout_us.load(std::memory_order_relaxed) * 100u; /* 100 MHz wall clock */
     t.stamps = g_stamps.load(std::memory_order_relaxed);
-    hipLaunchKernelGGL(k_resident, dim3(t.nblk), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
+    /* one selector workgroup per shared segment when they fit beside the chunks (one per CU):
+     * the segment's select runs on a CU that holds no chunk */
+    int nshared = 0;
+    for (int i = 0; i < t.nseg; ++i) nshared += t.s[i].n > RES_CHUNK;
+    t.nsel = 0;
+    if (nshared > 0 && t.nblk + nshared <= RES_MAX_WG && t.nblk + nshared <= resident_capacity())
+        for (int i = 0; i < t.nseg; ++i)
+            if (t.s[i].n > RES_CHUNK) t.sel_seg[t.nsel++] = i;
+    hipLaunchKernelGGL(k_resident, dim3(t.nblk + t.nsel), dim3(RES_THREADS), 0, s, t, head, cand, res, thr_out);
 }
 void launch_dwt_cols(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* L, float* H,
                      hipStream_t s) {

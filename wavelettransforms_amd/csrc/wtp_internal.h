@@ -97,13 +97,16 @@ struct SegDesc {
 struct SegTable {
     int32_t nseg;
     int32_t nblk;
-    int32_t pad[2];
+    int32_t nsel;      /* k_resident: selector workgroups after the nblk chunks (0: every segment selects for itself) */
+    int32_t pad;
     uint32_t res_timeout; /* k_resident: bound of every wait, in ticks of the 100 MHz wall clock */
     int32_t pad2;
     unsigned long long* stamps; /* k_resident: [0] min start, [1] max end (100 MHz ticks); null = off */
     int32_t blk_begin[SEG_PER_LAUNCH]; /* INT32_MAX past nseg: block -> segment in one scalar sweep */
+    int32_t sel_seg[SEG_PER_LAUNCH];   /* k_resident: the segment of selector j */
     SegDesc s[SEG_PER_LAUNCH];
 };
+static_assert(sizeof(SegTable) <= 4096, "k_resident's kernel argument");
 
 /* per-slot selection state.  Slots are the positions of a segment inside its launch group
  * (0..SEG_PER_LAUNCH-1); the SelState slots sit at the very start of every workspace
@@ -119,7 +122,9 @@ struct alignas(128) SelState {
     unsigned long long seg_bar[NSHARD]; /* k_resident: [0] = workgroups of the segment past a full-scan select */
     uint32_t maxkey[NSHARD];          /* atomicMax (k_collect)                               */
     uint32_t overflow;                /* a block had more inside keys than it can stage     */
-    uint32_t pad0[23];
+    uint32_t pad0a;
+    unsigned long long thr_gr;        /* k_resident: the selector's threshold granule {thr bits, RES_GR_* tag} */
+    uint32_t pad0[20];
     uint32_t kl, kh;                  /* window (k_collect); kh = 0xFFFFFFFF: unbounded      */
     uint32_t shift;                   /* bucket of an inside key = (key - kl - 1) >> shift   */
     int32_t mode;                     /* MODE_* chosen by the select (diagnostics)           */
@@ -214,6 +219,10 @@ void set_kernel_stamps(unsigned long long* dev); /* k_resident / k_small launch 
 uint32_t resident_timeout_us();
 unsigned long long* kernel_stamps();
 constexpr uint32_t RES_POISON = 0x80000000u; /* a segment barrier counter whose wait timed out */
+/* the tag of a selector's threshold granule (SelState::thr_gr, high word; 0 = not yet) */
+constexpr uint32_t RES_GR_OK = 1u;     /* the low word is the float32 threshold */
+constexpr uint32_t RES_GR_ALL = 2u;    /* the window missed: every float4 is rewritten */
+constexpr uint32_t RES_GR_FAULT = 4u;  /* a wait timed out: nobody stores */
 void launch_resident(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
                      hipStream_t s);
 /* ---- the small-population path in one launch (small.hip, k_small) ----

@@ -223,15 +223,19 @@ def set_resident(enabled):
 
 def set_pipeline(enabled):
     """Overlap each launch group's selection with the next group's forward transform on a side
-    stream (include/wtprune.h wtp_set_pipeline); returns the previous setting."""
-    return bool(N.lib().wtp_set_pipeline(1 if enabled else 0))
+    stream (True / 1, the default), or run every group on a lane stream of its own, staggered, with
+    the selections on the side stream (2); False / 0 one stream (include/wtprune.h
+    wtp_set_pipeline).  Returns the previous mode."""
+    mode = (1 if enabled else 0) if isinstance(enabled, bool) else int(enabled)
+    return int(N.lib().wtp_set_pipeline(mode))
 
 
 def set_interior(enabled):
-    """Filter-bank kernel choice (include/wtprune.h wtp_set_interior): True / 2 the interior tiles
-    and the frame around them in the edge-free kernels and their edge form (default), 1 the frame
-    in the general kernel, False / 0 every tile in the general kernel; returns the previous mode."""
-    mode = (2 if enabled else 0) if isinstance(enabled, bool) else int(enabled)
+    """Filter-bank kernel choice (include/wtprune.h wtp_set_interior): True / 3 the interior tiles
+    and the frame around them in the edge-free kernels and their edge form, one launch per level
+    (default), 2 the same as two launches, 1 the frame in the general kernel, False / 0 every tile
+    in the general kernel; returns the previous mode."""
+    mode = (3 if enabled else 0) if isinstance(enabled, bool) else int(enabled)
     return int(N.lib().wtp_set_interior(mode))
 
 
