@@ -567,11 +567,13 @@ def main():
                                     "bytes_received_max_rank": max(plan.bytes_received(r) for r in range(world)),
                                     "largest_region_bytes": 4 * max(plan.size),
                                     "per_link_estimate_us": 4 * max(plan.size) / XGMI_LINK_GBS / 1e3,
-                                    "exchange_status": "batch_isend_irecv over RCCL at N > 1 had not run on hardware "
-                                                       "before this line (covered by world-2/3 gloo and a world-1 "
-                                                       "RCCL group); per_link_estimate_us assumes every peer pair on "
-                                                       "its own xGMI link at %.0f GB/s, the largest region the "
-                                                       "longest copy" % XGMI_LINK_GBS,
+                                    "exchange_status": (("rehearsal: batch_isend_irecv over %s with every rank on one "
+                                                         "GPU, a functional check; RCCL at N > 1 is not measured by "
+                                                         "this line" % dist.get_backend()) if rehearsal else
+                                                        ("batch_isend_irecv over %s (RCCL on ROCm) across %d GPUs, "
+                                                         "measured by this line" % (dist.get_backend(), world))),
+                                    "per_link_estimate_note": "assumes every peer pair on its own xGMI link at %.0f "
+                                                              "GB/s, the largest region the longest copy" % XGMI_LINK_GBS,
                                     "note": "LPT layer shards pruned in place into the flat state_dict buffer, then "
                                             "ONE full-mesh exchange of the unpadded regions (weights + records; "
                                             "batch_isend_irecv = one RCCL group of point-to-point copies, one per "

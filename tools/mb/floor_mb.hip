@@ -17,7 +17,7 @@ constexpr int NSEG = 20;
 __constant__ int c_wgs[NSEG] = {1, 1, 1, 1, 1, 1, 2, 3, 3, 3, 1, 6, 12, 12, 12, 3, 24, 48, 48, 48};
 constexpr uint64_t TMO = 2000000; /* 20 ms of the 100 MHz clock */
 
-enum { SPEC = 1, REMOTE = 2, NOCHAIN = 4, COPY = 8, NOPUB = 16, SPECALL = 32 };
+enum { SPEC = 1, REMOTE = 2, NOCHAIN = 4, COPY = 8, NOPUB = 16, SPECALL = 32, SAMPLE = 64, READONLY = 128 };
 
 __device__ __forceinline__ uint32_t ldc(const uint32_t* p) { return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void stc(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -90,6 +90,7 @@ __global__ __launch_bounds__(CT) void k_sched(const float* __restrict__ x, float
         while (b >= b0 + c_wgs[seg]) { b0 += c_wgs[seg]; ++seg; }
     }
     const bool selector = b >= nchunks;
+    const int nwg = selector ? 0 : c_wgs[seg];
     if (selector) {
         /* selector of the multi-workgroup segment number (b - nchunks) */
         int m = b - nchunks, s = 0, sb = 0;
@@ -102,13 +103,31 @@ __global__ __launch_bounds__(CT) void k_sched(const float* __restrict__ x, float
         if (tid == 0) atomicMax(stamps + 1, ticks());
         return;
     }
-    const int nwg = c_wgs[seg];
     const float4* x4 = reinterpret_cast<const float4*>(x + (int64_t)b * CHUNK);
     float4* y4 = reinterpret_cast<float4*>(y + (int64_t)b * CHUNK);
     float4 v[IT];
+    uint32_t smp = 0;
+    if ((mode & SAMPLE) && tid < 256) {
+        /* k_resident's sample: 16 loads a lane, groups of 16 contiguous floats spread over the
+         * segment, issued ahead of the chunk */
+        const float* sx = x + (int64_t)b0 * CHUNK;
+        const int64_t n = (int64_t)nwg * CHUNK;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int i = j * 256 + tid;
+            const int64_t pos = (int64_t)(i / 16) * ((n - 16) / 255) + (i % 16);
+            smp += __float_as_uint(sx[pos]);
+        }
+    }
+    __syncthreads();
 #pragma unroll
     for (int it = 0; it < IT; ++it) v[it] = x4[it * CT + tid];
-    if (mode & COPY) {
+    if (mode & READONLY) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) sacc += v[it].x + v[it].y + v[it].z + v[it].w;
+        if (sacc == 1234.5f + (float)smp) y[tid] = sacc;
+    } else if (mode & COPY) {
 #pragma unroll
         for (int it = 0; it < IT; ++it) y4[it * CT + tid] = v[it];
     } else {
@@ -189,7 +208,11 @@ int main(int argc, char** argv) {
     CK(hipFuncSetAttribute((const void*)k_sched, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     uint32_t epoch = 0;
     struct V { const char* name; int mode; };
-    const V vs[] = {{"copy (no barrier)", COPY},
+    const V vs[] = {{"read only", READONLY},
+                    {"read only, sample first", READONLY | SAMPLE},
+                    {"copy (no barrier)", COPY},
+                    {"copy, sample first", COPY | SAMPLE},
+                    {"read, barrier, write, sample first", NOCHAIN | NOPUB | SAMPLE},
                     {"read, barrier, write (no chain)", NOCHAIN | NOPUB},
                     {"read, pub, barrier, write", NOCHAIN},
                     {"local chain (k_resident form)", 0},

@@ -88,16 +88,39 @@ def lib():
             "wtp_last_error": ([], ctypes.c_char_p),
             "wtp_last_error_tensor": ([], i32),
         }
+        missing = {}
         for name, (args, ret) in sigs.items():
             if os.environ.get("WTP_LIB_PATH") and not hasattr(L, name):
-                continue  # an A/B lab build of an older revision: entry points added since are absent
+                # an A/B lab build of an older revision: entry points added since are absent; a
+                # call to one raises an error that names it (not a bare AttributeError)
+                missing[name] = _missing_entry(name)
+                continue
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = ret
         if L.wtp_abi_version() != 1:
             raise NativeLibraryMissing("libwtprune.so ABI version mismatch")
-        _lib = L
+        _lib = _LabLib(L, missing) if missing else L
     return _lib
+
+
+def _missing_entry(name):
+    def call(*_a, **_k):
+        raise NativeLibraryMissing("%s (WTP_LIB_PATH) has no entry point %s: it was built from an older "
+                                   "revision" % (LIB_PATH, name))
+    return call
+
+
+class _LabLib:
+    """A lab library (WTP_LIB_PATH) with the entry points it lacks replaced by stubs that raise."""
+
+    def __init__(self, L, missing):
+        self._L, self._missing = L, missing
+
+    def __getattr__(self, name):
+        if name in self._missing:
+            return self._missing[name]
+        return getattr(self._L, name)
 
 
 def exported_symbols():

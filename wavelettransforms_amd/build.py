@@ -13,7 +13,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(OUT_DIR, "libwtprune.so")
 SOURCES = ["kernels.hip", "filterbank.hip", "small.hip", "api.hip"]
-DEPS = SOURCES + ["wtp_internal.h", "wt_dwt_core.h", "wt_synth.h", "wt_perm.h", "wt_filters.inc", "small_geom.h"]
+DEPS = SOURCES + ["wtp_internal.h", "wt_dwt_core.h", "wt_synth.h", "wt_perm.h", "wt_filters.inc", "small_geom.h", "fb_index.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("WTP_OFFLOAD_ARCH", "gfx950")
 

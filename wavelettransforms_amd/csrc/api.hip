@@ -796,8 +796,11 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap, p.dwt);
             if (resident) {
                 sd.nsub_log2 = RES_NSUB_LOG2;
-                if (p.pop > RES_MS)
-                    sd.res_step_fx = ((uint64_t)(p.pop - SAMPLE_GROUP) << 32) / (uint64_t)(RES_MS / SAMPLE_GROUP - 1);
+                if (p.pop > RES_MS) /* rounded up: floor(g * step_fx / 2^32) is then the exact floor of
+                                       * g (n - 16) / 255 for every group g <= 255 (the error stays
+                                       * below 255 / 2^32, under the 1/255 gap to the next integer) */
+                    sd.res_step_fx = (((uint64_t)(p.pop - SAMPLE_GROUP) << 32) + (uint64_t)(RES_MS / SAMPLE_GROUP - 2)) /
+                                     (uint64_t)(RES_MS / SAMPLE_GROUP - 1);
             }
             if (late[t - g0]) sd.flags |= SEG_LATE;
             blk += (int)((p.pop + chunk - 1) / chunk);

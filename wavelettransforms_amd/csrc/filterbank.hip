@@ -19,6 +19,7 @@
  */
 #include "wtp_internal.h"
 #include "wt_dwt_core.h"
+#include "fb_index.h"
 
 #include <algorithm>
 #include <atomic>
@@ -56,15 +57,6 @@ constexpr int FB_MAX_LDS = 64 * 1024;
 template <int FT> constexpr int FWD_S0 = ((1 - FT / 2) % 4 + 4) % 4;
 template <int FT> constexpr int FWD_TP = (FWD_S0<FT> + 2 * FC + FT - 2 + 3) / 4 * 4;
 
-/* XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (blocks b and b+8
- * share one L2), so tile t = xcd * per + b / 8 gives each XCD a contiguous run of tiles and the
- * halos neighbouring tiles re-read come from that XCD's L2 (MI355X_MICROARCH.md, XCD placement;
- * placement is a speed matter only, never correctness) */
-__device__ __forceinline__ int xcd_tile(int b, int n) {
-    const int per = (n + 7) / 8, x = b & 7, k = b >> 3;
-    const int full = n - 8 * (per - 1); /* XCDs that get `per` tiles; the rest get per - 1 */
-    return x < full ? x * per + k : full * per + (x - full) * (per - 1) + k;
-}
 
 __device__ __forceinline__ int ext_idx(int t, int N) { /* wt_ext_index in 32 bits */
     const int Ne = N + (N & 1);
@@ -276,24 +268,6 @@ struct FwdArgs {
  * a block's item is its tile / tiles-per-item.  The specialised kernels take their taps as a
  * SmallTaps (F <= 20): the whole argument stays near 2 KB. */
 constexpr int FB_UNI = 64;
-/* division by a launch-invariant d on the scalar unit (Granlund-Montgomery, exact for every 32-bit
- * n): the tile decode's quotients are uniform, and the compiler's own division expands to a
- * float reciprocal sequence on the VALU of every wave */
-struct FastDiv {
-    uint32_t m, sh; /* sh: first shift (0 or 1) | second shift << 8 */
-};
-__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
-    const uint32_t u = (uint32_t)n, t = __umulhi(u, f.m);
-    return (int)((t + ((u - t) >> (f.sh & 0xFFu))) >> (f.sh >> 8));
-}
-static inline FastDiv make_fastdiv(uint32_t d) {
-    int l = 0;
-    while (l < 32 && (1ull << l) < d) ++l;
-    FastDiv f;
-    f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
-    f.sh = l ? (1u | ((uint32_t)(l - 1) << 8)) : 0u;
-    return f;
-}
 struct FwdGroup {
     FwdArgs geo;            /* the items' geometry; its pointers are unused */
     int n, tiles;           /* items; tiles per item */
@@ -309,49 +283,6 @@ struct FwdGroup {
 };
 template <int FT> using TapsT = typename std::conditional<FT == 0, Taps, SmallTaps>::type;
 
-/* frame index f -> tile (tr, tc) of a grid of tilesC columns around the interior rectangle
- * [r0, r0 + nr) x [c0, c0 + nc): the rows above it, then the side tiles of its rows, then the
- * rows below it (row-major inside each part) */
-__device__ __forceinline__ void frame_tile(int f, int tilesC, int r0, int nr, int c0, int nc, int* tr, int* tc) {
-    const int top = r0 * tilesC, side = tilesC - nc;
-    if (f < top) {
-        *tr = f / tilesC;
-        *tc = f - *tr * tilesC;
-        return;
-    }
-    f -= top;
-    if (f < nr * side) {
-        const int q = f / side, k = f - q * side;
-        *tr = r0 + q;
-        *tc = k < c0 ? k : k + nc;
-        return;
-    }
-    f -= nr * side;
-    *tr = r0 + nr + f / tilesC;
-    *tc = f - (f / tilesC) * tilesC;
-}
-
-/* frame_tile with the divisions by tilesC and tilesC - nc on the scalar unit */
-__device__ __forceinline__ void frame_tile_fd(int f, int tilesC, int r0, int nr, int c0, int nc, const FastDiv& dtc,
-                                              const FastDiv& dside, int* tr, int* tc) {
-    const int top = r0 * tilesC, side = tilesC - nc;
-    if (f < top) {
-        *tr = fdiv(f, dtc);
-        *tc = f - *tr * tilesC;
-        return;
-    }
-    f -= top;
-    if (f < nr * side) {
-        const int q = fdiv(f, dside), k = f - q * side;
-        *tr = r0 + q;
-        *tc = k < c0 ? k : k + nc;
-        return;
-    }
-    f -= nr * side;
-    const int q = fdiv(f, dtc);
-    *tr = r0 + nr + q;
-    *tc = f - q * tilesC;
-}
 
 /* taps of the interior kernels: analysis {dec_lo[j], dec_hi[j]} adjacent, so one SGPR pair is
  * both bands' packed tap */
