@@ -191,10 +191,11 @@ unsigned wtp_set_resident_timeout_us(unsigned us);
  * the previous mode (process-wide). */
 int wtp_set_pipeline(int mode);
 /* The filter-bank levels run their interior tiles (input window inside the image, full tile)
- * in kernels compiled without the edge forms.  Mode 3 (default): the frame of edge tiles in the
- * same kernels' edge-capable form, in the same launch as the interior; mode 2: the same as two
- * launches; mode 1: the frame in the general kernel; mode 0: every tile in the general kernel
- * (identical results in every mode).  Returns the previous mode (process-wide). */
+ * in kernels compiled without the edge forms and the frame of edge tiles in the same kernels'
+ * edge-capable form (mode 2); mode 3 (default) as 2, but a small level (a few thousand tiles)
+ * runs every tile in one launch of the edge-capable form; mode 1: the frame in the general
+ * kernel; mode 0: every tile in the general kernel (identical results in every mode).  Returns the
+ * previous mode (process-wide). */
 int wtp_set_interior(int mode);
 #define WTP_PATH_SMALL 4 /* every tensor of the call ran in one launch (2-D transforms, small population) */
 /* measurement hook (bench.py): while set, every resident launch atomically lowers stamps_dev[0] to

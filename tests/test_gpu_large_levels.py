@@ -47,8 +47,8 @@ def test_large_levels_equal_oracle(wavelet):
 @pytest.mark.parametrize("wavelet", WAVELETS)
 def test_interior_kernels_equal_general(wavelet):
     """The interior filter-bank kernels (k_fwd_int / k_inv_int) with the frame of edge tiles in
-    their EDGE form, in the interior's launch (mode 3, the default) or in a launch of its own (mode
-    2), and in the general kernels (mode 1), against every tile
+    their EDGE form (mode 2; mode 3, the default, runs the small levels' every tile in the EDGE
+    form), and in the general kernels (mode 1), against every tile
     in the general kernels (mode 0): packed coefficients and pruned outputs bit for bit, on shapes
     with an interior and a frame (odd extents, batches, partial last tiles, a 2-level and a 4-level
     tree; the deepest levels of the narrow shape fall back to the general frame)."""

@@ -148,6 +148,23 @@ def test_more_segments_than_one_group(eng, mode):
         _same(o.cpu().numpy(), ref, r, rr)
 
 
+@pytest.mark.parametrize("in_place", [False, True], ids=["out_of_place", "in_place"])
+def test_shared_segments_without_room_for_selectors(eng, in_place):
+    """24 shared segments of 10 workgroups each: 240 chunks leave no room for the 24 selector
+    workgroups beside them (one per CU), so every segment selects for itself (the local chain);
+    beside the selector form on cfg2, the same results."""
+    cap = eng.resident_capacity()
+    n = 10 * RES_CHUNK - 3
+    xs = [eng.synth((n,), 41, j, 27 + (j % 3)) for j in range(24)]
+    assert 24 * 10 <= cap < 24 * 10 + 24
+    hosts = [x.cpu().numpy() for x in xs]
+    outs, res = eng.prune(xs, "bior3.3", 5, 61.8, outs=xs if in_place else None, carry_level=False)
+    for h, o, r in zip(hosts, outs, res):
+        ref, rr = O.prune_tensor(h, "bior3.3", 5, 61.8)
+        _same(o.cpu().numpy(), ref, r, rr)
+        assert r["path"] in (1, 2)
+
+
 def test_group_larger_than_resident_grid_falls_back(eng):
     """A level-0 group needing more workgroups than resident_capacity() runs the three-launch
     form (same results)."""

@@ -690,9 +690,11 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     int dwt_groups = 0;
     for (const auto& gc : gchains) dwt_groups += !gc.empty();
     const int pmode = dwt_groups > 1 ? g_pipeline.load(std::memory_order_relaxed) : 0;
-    /* mode 2 (lanes): events [0] the fork, per group g at 1 + 4 g: the forward's stagger mark,
-     * forward done, selection done, lane done; the side stream's end last */
-    const int nev = pmode == 2 ? 2 + 4 * ngroups : 2 * ngroups + 1;
+    /* mode 2 (lanes): events [0] the fork, per group g at 1 + 7 g: the forward's stagger mark,
+     * forward done, selection done, lane done, and the caller's-stream relays of the first three
+     * (EV_*); the side stream's end last */
+    enum { EV_MARK = 1, EV_FDONE, EV_SDONE, EV_LDONE, EV_MARK_R, EV_FDONE_R, EV_SDONE_R, EV_PER = 7 };
+    const int nev = pmode == 2 ? 2 + EV_PER * ngroups : 2 * ngroups + 1;
     SidePipe* pipe = pmode ? side_pipe(s, nev, pmode == 2 ? ngroups : 0) : nullptr;
     const bool lanes = pipe && pmode == 2;
     const hipStream_t ss = pipe ? pipe->side : s; /* the selection's stream */
@@ -706,8 +708,8 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             (void)hipStreamWaitEvent(s, e, 0);
             if (lanes)
                 for (int gi = 0; gi < ngroups; ++gi) {
-                    (void)hipEventRecord(pipe->ev[4 + 4 * gi], pipe->lanes[gi]);
-                    (void)hipStreamWaitEvent(s, pipe->ev[4 + 4 * gi], 0);
+                    (void)hipEventRecord(pipe->ev[EV_LDONE + EV_PER * gi], pipe->lanes[gi]);
+                    (void)hipStreamWaitEvent(s, pipe->ev[EV_LDONE + EV_PER * gi], 0);
                 }
         }
         return fail(WTP_EHIP, t, "%s", msg);
@@ -716,19 +718,29 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
      * done, so one group's latency-bound small levels and its selection run beside the next group's
      * large ones */
     constexpr int FB_STAGGER = 2;
+    /* Every dependency between two forked streams is relayed through the caller's stream: it waits
+     * for the producer's event and records a relay event the consumer waits for.  A captured graph
+     * whose side stream waits on a lane's event while that lane waits on the side stream's (the
+     * direct form) segfaults in hipStreamEndCapture on ROCm 7.2 -- reproduced with plain torch
+     * streams and no kernel of ours (tools/lanes_capture_diag.py, torch_side_lane_cross); forked
+     * streams that wait only on the capturing stream's events are the form mode 1 always used. */
+    auto relay = [&](hipEvent_t producer, hipEvent_t r) {
+        return hipStreamWaitEvent(s, producer, 0) == hipSuccess && hipEventRecord(r, s) == hipSuccess;
+    };
     if (lanes) {
         if (hipEventRecord(pipe->ev[0], s) != hipSuccess) return fail(WTP_EHIP, -1, "hipEventRecord failed");
         forked = true;
         if (hipStreamWaitEvent(ss, pipe->ev[0], 0) != hipSuccess) return fail_joined(-1, "hipStreamWaitEvent failed");
-        int prev = -1;
+        hipEvent_t start = pipe->ev[0];
         for (int gi = 0; gi < ngroups; ++gi) {
             const hipStream_t L = pipe->lanes[gi];
-            if (hipStreamWaitEvent(L, pipe->ev[prev < 0 ? 0 : 1 + 4 * prev], 0) != hipSuccess)
-                return fail_joined(-1, "hipStreamWaitEvent failed");
+            hipEvent_t* e = pipe->ev.data() + EV_PER * gi;
+            if (hipStreamWaitEvent(L, start, 0) != hipSuccess) return fail_joined(-1, "hipStreamWaitEvent failed");
             if (gchains[gi].empty()) continue;
-            forward_chains(gchains[gi], tp, L, FB_STAGGER, pipe->ev[1 + 4 * gi]);
-            if (hipEventRecord(pipe->ev[2 + 4 * gi], L) != hipSuccess) return fail_joined(-1, "hipEventRecord failed");
-            prev = gi;
+            forward_chains(gchains[gi], tp, L, FB_STAGGER, e[EV_MARK]);
+            if (hipEventRecord(e[EV_FDONE], L) != hipSuccess) return fail_joined(-1, "hipEventRecord failed");
+            if (!relay(e[EV_MARK], e[EV_MARK_R])) return fail_joined(-1, "relay failed");
+            start = e[EV_MARK_R];
         }
     }
     if (!pipe) forward_chains(chains, tp, s);
@@ -738,8 +750,10 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     for (int g0 = 0; g0 < ntensors; g0 += SEG_PER_LAUNCH) {
         const int g1 = std::min(ntensors, g0 + SEG_PER_LAUNCH);
         const int gi = g0 / SEG_PER_LAUNCH;
-        if (lanes) { /* this group's selection behind its forward (on its lane) */
-            if (!gchains[gi].empty() && hipStreamWaitEvent(ss, pipe->ev[2 + 4 * gi], 0) != hipSuccess)
+        if (lanes) { /* this group's selection behind its forward (on its lane), relayed */
+            hipEvent_t* e = pipe->ev.data() + EV_PER * gi;
+            if (!gchains[gi].empty() &&
+                (!relay(e[EV_FDONE], e[EV_FDONE_R]) || hipStreamWaitEvent(ss, e[EV_FDONE_R], 0) != hipSuccess))
                 return fail_joined(-1, "hipStreamWaitEvent failed");
         } else if (pipe) { /* this group's forward levels on the caller's stream, its selection behind them */
             forward_chains(gchains[gi], tp, s);
@@ -826,8 +840,10 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         if (lanes) { /* the group's inverse on its lane behind its selection; the lane joins the caller's stream */
             if (!gchains[gi].empty()) {
                 const hipStream_t L = pipe->lanes[gi];
-                if (hipEventRecord(pipe->ev[3 + 4 * gi], ss) != hipSuccess) return fail_joined(-1, "hipEventRecord failed");
-                if (hipStreamWaitEvent(L, pipe->ev[3 + 4 * gi], 0) != hipSuccess)
+                hipEvent_t* e = pipe->ev.data() + EV_PER * gi;
+                if (hipEventRecord(e[EV_SDONE], ss) != hipSuccess || !relay(e[EV_SDONE], e[EV_SDONE_R]))
+                    return fail_joined(-1, "hipEventRecord failed");
+                if (hipStreamWaitEvent(L, e[EV_SDONE_R], 0) != hipSuccess)
                     return fail_joined(-1, "hipStreamWaitEvent failed");
                 inverse_chains(gchains[gi], tp, L);
             }
@@ -837,8 +853,8 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     }
     if (lanes) { /* every lane and the side stream back into the caller's stream */
         for (int gi = 0; gi < ngroups; ++gi) {
-            if (hipEventRecord(pipe->ev[4 + 4 * gi], pipe->lanes[gi]) != hipSuccess ||
-                hipStreamWaitEvent(s, pipe->ev[4 + 4 * gi], 0) != hipSuccess)
+            if (hipEventRecord(pipe->ev[EV_LDONE + EV_PER * gi], pipe->lanes[gi]) != hipSuccess ||
+                hipStreamWaitEvent(s, pipe->ev[EV_LDONE + EV_PER * gi], 0) != hipSuccess)
                 return fail(WTP_EHIP, -1, "lane join failed");
         }
         if (hipEventRecord(pipe->ev[nev - 1], ss) != hipSuccess || hipStreamWaitEvent(s, pipe->ev[nev - 1], 0) != hipSuccess)

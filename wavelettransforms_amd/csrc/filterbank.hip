@@ -273,10 +273,6 @@ struct FwdGroup {
     int n, tiles;           /* items; tiles per item */
     FastDiv dv_tiles, dv_per, dv_ntc; /* k_*_int: by tiles, by the rectangle's (or frame's) tiles, by nTC */
     FastDiv dv_tc, dv_side;           /* the frame's decode: by tilesC, by tilesC - nTC */
-    /* a merged launch (k_fwd_int<FT, FB_BOTH>): blocks [0, nblk_f) are the frame's tiles_f tiles
-     * per item, the rest the interior's */
-    int nblk_f, tiles_f;
-    FastDiv dvf_tiles, dvf_per;
     const float* in[FB_UNI];
     float* anext[FB_UNI];
     float* P[FB_UNI];
@@ -289,10 +285,7 @@ template <int FT> using TapsT = typename std::conditional<FT == 0, Taps, SmallTa
 struct FwdIntTaps {
     f2 t[SM_F_MAX];
 };
-/* KIND of an interior-kernel launch: the interior rectangle's tiles, the frame's, or both in one
- * grid (the frame's blocks first: its tiles are the slower ones) */
-enum FbKind { FB_INT = 0, FB_FRAME = 1, FB_BOTH = 2 };
-#define WTP_FB_INT_WPE __attribute__((amdgpu_waves_per_eu(KIND != FB_INT ? 5 : 6))) /* edge forms: room */
+#define WTP_FB_INT_WPE __attribute__((amdgpu_waves_per_eu(EDGE ? 5 : 6))) /* EDGE: room for the edge forms */
 
 template <int FT>
 __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGroup g, TapsT<FT> tp) {
@@ -521,8 +514,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
  *   row pass: as k_fwd_level's interior form; stores by buffer instructions whose row offset is a
  *   scalar (the row is wave-uniform) and column offset the lane's -- no 64-bit address math. */
 template <int FT, bool EDGE>
-__device__ __forceinline__ void fwd_int_body(const FwdGroup& g, const FwdIntTaps& tp, int blk, int nblk, int tiles,
-                                             const FastDiv& dvt, const FastDiv& dvp) {
+__global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup g, FwdIntTaps tp) {
     static_assert(FT > 0 && FT % 2 == 0, "specialised even filters");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int NRc = 2 * FR + FT - 2, NCc = 2 * FC + FT - 2;
@@ -530,18 +522,18 @@ __device__ __forceinline__ void fwd_int_body(const FwdGroup& g, const FwdIntTaps
     constexpr int HALF = (NCc + 1) / 2;
     float* T = lds;
     float2* LH = reinterpret_cast<float2*>(lds);
-    const int gt = xcd_tile(blk, nblk);
-    const int item = fdiv(gt, dvt);
+    const int gt = xcd_tile(blockIdx.x, gridDim.x);
+    const int item = fdiv(gt, g.dv_tiles);
     const FwdArgs& a = g.geo;
-    const int tile = gt - item * tiles;
+    const int tile = gt - item * g.tiles;
     int b, trow, tcol;
     if constexpr (EDGE) {
         const int per = a.tilesR * a.tilesC - a.nTR * a.nTC;
-        b = fdiv(tile, dvp);
+        b = fdiv(tile, g.dv_per);
         frame_tile_fd(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, g.dv_tc, g.dv_side, &trow, &tcol);
     } else {
         const int per = a.nTR * a.nTC;
-        b = fdiv(tile, dvp);
+        b = fdiv(tile, g.dv_per);
         const int t2 = tile - b * per, trr = fdiv(t2, g.dv_ntc);
         trow = a.tr0 + trr;
         tcol = a.tc0 + t2 - trr * a.nTC;
@@ -739,19 +731,6 @@ __device__ __forceinline__ void fwd_int_body(const FwdGroup& g, const FwdIntTaps
     WTP_FPROBE(3);
 }
 
-template <int FT, int KIND>
-__global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup g, FwdIntTaps tp) {
-    if constexpr (KIND == FB_INT) {
-        fwd_int_body<FT, false>(g, tp, blockIdx.x, gridDim.x, g.tiles, g.dv_tiles, g.dv_per);
-    } else if constexpr (KIND == FB_FRAME) {
-        fwd_int_body<FT, true>(g, tp, blockIdx.x, gridDim.x, g.tiles_f, g.dvf_tiles, g.dvf_per);
-    } else if ((int)blockIdx.x < g.nblk_f) { /* block-uniform */
-        fwd_int_body<FT, true>(g, tp, blockIdx.x, g.nblk_f, g.tiles_f, g.dvf_tiles, g.dvf_per);
-    } else {
-        fwd_int_body<FT, false>(g, tp, blockIdx.x - g.nblk_f, gridDim.x - g.nblk_f, g.tiles, g.dv_tiles, g.dv_per);
-    }
-}
-
 /* ------------------------------------------------------------ synthesis --- */
 struct InvArgs {
     const float* a;      /* approximation (B, R, C) with row pitch lda, batch stride a_bs */
@@ -779,8 +758,6 @@ struct InvGroup {
     int n, tiles;
     FastDiv dv_tiles, dv_per, dv_ntc; /* as FwdGroup */
     FastDiv dv_tc, dv_side;
-    int nblk_f, tiles_f;
-    FastDiv dvf_tiles, dvf_per;
     const float* a[FB_UNI];
     const float* P[FB_UNI];
     float* y[FB_UNI];
@@ -1088,24 +1065,23 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INV_WPE void k_inv_level(InvGrou
  * taps are register pairs broadcast by op_sel, the output stores take the row as a scalar
  * offset, and zeros are counted by ballot. */
 template <int FT, bool EDGE>
-__device__ __forceinline__ void inv_int_body(const InvGroup& g, const SmallTaps& tp, int blk, int nblk, int tiles,
-                                             const FastDiv& dvt, const FastDiv& dvp) {
+__global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup g, SmallTaps tp) {
     static_assert(FT > 0 && FT % 2 == 0, "specialised even filters");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int H = FT / 2, HM = H;
     constexpr int NR = IR / 2 + H - (H & 1), NC = IC / 2 + H - (H & 1); /* coefficient rows / columns */
-    const int gt = xcd_tile(blk, nblk);
-    const int item = fdiv(gt, dvt);
+    const int gt = xcd_tile(blockIdx.x, gridDim.x);
+    const int item = fdiv(gt, g.dv_tiles);
     const InvArgs& a = g.geo;
-    const int tile = gt - item * tiles;
+    const int tile = gt - item * g.tiles;
     int b, trow, tcol;
     if constexpr (EDGE) {
         const int per = a.tilesR * a.tilesC - a.nTR * a.nTC;
-        b = fdiv(tile, dvp);
+        b = fdiv(tile, g.dv_per);
         frame_tile_fd(tile - b * per, a.tilesC, a.tr0, a.nTR, a.tc0, a.nTC, g.dv_tc, g.dv_side, &trow, &tcol);
     } else {
         const int per = a.nTR * a.nTC;
-        b = fdiv(tile, dvp);
+        b = fdiv(tile, g.dv_per);
         const int t2 = tile - b * per, trr = fdiv(t2, g.dv_ntc);
         trow = a.tr0 + trr;
         tcol = a.tc0 + t2 - trr * a.nTC;
@@ -1344,23 +1320,13 @@ __device__ __forceinline__ void inv_int_body(const InvGroup& g, const SmallTaps&
     WTP_FPROBE(3);
 }
 
-template <int FT, int KIND>
-__global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup g, SmallTaps tp) {
-    if constexpr (KIND == FB_INT) {
-        inv_int_body<FT, false>(g, tp, blockIdx.x, gridDim.x, g.tiles, g.dv_tiles, g.dv_per);
-    } else if constexpr (KIND == FB_FRAME) {
-        inv_int_body<FT, true>(g, tp, blockIdx.x, gridDim.x, g.tiles_f, g.dvf_tiles, g.dvf_per);
-    } else if ((int)blockIdx.x < g.nblk_f) { /* block-uniform */
-        inv_int_body<FT, true>(g, tp, blockIdx.x, g.nblk_f, g.tiles_f, g.dvf_tiles, g.dvf_per);
-    } else {
-        inv_int_body<FT, false>(g, tp, blockIdx.x - g.nblk_f, gridDim.x - g.nblk_f, g.tiles, g.dv_tiles, g.dv_per);
-    }
-}
-
 /* ------------------------------------------------------------ launchers --- */
-/* which kernels run a level's tiles: 2 (default) the interior rectangle in k_fwd_int / k_inv_int and
- * the frame around it in their EDGE forms; 1 the frame in the general k_fwd_level / k_inv_level;
- * 0 every tile in the general kernels (A/B and parity cross-checks) */
+/* which kernels run a level's tiles: 3 (default) as 2, except that a level of at most
+ * FB_ONE_LAUNCH_TILES tiles (all items of the launch) runs every tile in ONE launch of the EDGE
+ * form; 2 the interior rectangle in k_fwd_int / k_inv_int and the frame around it in their EDGE
+ * forms (two launches); 1 the frame in the general k_fwd_level / k_inv_level; 0 every tile in the
+ * general kernels (A/B and parity cross-checks) */
+constexpr int64_t FB_ONE_LAUNCH_TILES = 8192;
 static std::atomic<int> g_fb_interior{3};
 int fb_set_interior(int mode) { return g_fb_interior.exchange(mode < 0 ? 0 : (mode > 3 ? 3 : mode)); }
 
@@ -1397,12 +1363,12 @@ static void fwd_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
     static_assert(FT <= SM_F_MAX, "SmallTaps holds the specialised filters");
     hipLaunchKernelGGL(k_fwd_level<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, FT > 0), s, g, taps_of<FT>(tp));
 }
-template <int FT, int KIND>
+template <int FT, bool EDGE>
 static void fwd_int_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
     FwdIntTaps t;
     memset(&t, 0, sizeof t);
     for (int j = 0; j < FT; ++j) t.t[j] = f2{tp.f[0][j], tp.f[1][j]};
-    hipLaunchKernelGGL((k_fwd_int<FT, KIND>), dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, true), s, g, t);
+    hipLaunchKernelGGL((k_fwd_int<FT, EDGE>), dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, true), s, g, t);
 }
 
 /* The interior rectangle of a forward level's tile grid (k_fwd_int's tiles): a tile row is
@@ -1433,9 +1399,9 @@ template <int FT>
 static void inv_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
     hipLaunchKernelGGL(k_inv_level<FT>, dim3(grid), dim3(FB_THREADS), inv_lds(tp.F, FT > 0), s, g, taps_of<FT>(tp));
 }
-template <int FT, int KIND>
+template <int FT, bool EDGE>
 static void inv_int_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
-    hipLaunchKernelGGL((k_inv_int<FT, KIND>), dim3(grid), dim3(FB_THREADS), inv_lds(tp.F, true), s, g, taps_of<FT>(tp));
+    hipLaunchKernelGGL((k_inv_int<FT, EDGE>), dim3(grid), dim3(FB_THREADS), inv_lds(tp.F, true), s, g, taps_of<FT>(tp));
 }
 
 /* The interior rectangle of a synthesis level's tile grid (k_inv_int's tiles): along each axis a
@@ -1567,17 +1533,17 @@ static void fwd_general(const FwdGroup& g, int grid, const Taps& tp, hipStream_t
     default: fwd_go<0>(g, grid, tp, s); break;
     }
 }
-template <int KIND>
+template <bool EDGE>
 static void fwd_interior_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
     switch (tp.F) {
-    case 2: fwd_int_go<2, KIND>(g, grid, tp, s); break;
-    case 4: fwd_int_go<4, KIND>(g, grid, tp, s); break;
-    case 6: fwd_int_go<6, KIND>(g, grid, tp, s); break;
-    case 8: fwd_int_go<8, KIND>(g, grid, tp, s); break;
-    case 10: fwd_int_go<10, KIND>(g, grid, tp, s); break;
-    case 12: fwd_int_go<12, KIND>(g, grid, tp, s); break;
-    case 16: fwd_int_go<16, KIND>(g, grid, tp, s); break;
-    case 18: fwd_int_go<18, KIND>(g, grid, tp, s); break;
+    case 2: fwd_int_go<2, EDGE>(g, grid, tp, s); break;
+    case 4: fwd_int_go<4, EDGE>(g, grid, tp, s); break;
+    case 6: fwd_int_go<6, EDGE>(g, grid, tp, s); break;
+    case 8: fwd_int_go<8, EDGE>(g, grid, tp, s); break;
+    case 10: fwd_int_go<10, EDGE>(g, grid, tp, s); break;
+    case 12: fwd_int_go<12, EDGE>(g, grid, tp, s); break;
+    case 16: fwd_int_go<16, EDGE>(g, grid, tp, s); break;
+    case 18: fwd_int_go<18, EDGE>(g, grid, tp, s); break;
     default: break;
     }
 }
@@ -1594,17 +1560,17 @@ static void inv_general(const InvGroup& g, int grid, const Taps& tp, hipStream_t
     default: inv_go<0>(g, grid, tp, s); break;
     }
 }
-template <int KIND>
+template <bool EDGE>
 static void inv_interior_go(const InvGroup& g, int grid, const Taps& tp, hipStream_t s) {
     switch (tp.F) {
-    case 2: inv_int_go<2, KIND>(g, grid, tp, s); break;
-    case 4: inv_int_go<4, KIND>(g, grid, tp, s); break;
-    case 6: inv_int_go<6, KIND>(g, grid, tp, s); break;
-    case 8: inv_int_go<8, KIND>(g, grid, tp, s); break;
-    case 10: inv_int_go<10, KIND>(g, grid, tp, s); break;
-    case 12: inv_int_go<12, KIND>(g, grid, tp, s); break;
-    case 16: inv_int_go<16, KIND>(g, grid, tp, s); break;
-    case 18: inv_int_go<18, KIND>(g, grid, tp, s); break;
+    case 2: inv_int_go<2, EDGE>(g, grid, tp, s); break;
+    case 4: inv_int_go<4, EDGE>(g, grid, tp, s); break;
+    case 6: inv_int_go<6, EDGE>(g, grid, tp, s); break;
+    case 8: inv_int_go<8, EDGE>(g, grid, tp, s); break;
+    case 10: inv_int_go<10, EDGE>(g, grid, tp, s); break;
+    case 12: inv_int_go<12, EDGE>(g, grid, tp, s); break;
+    case 16: inv_int_go<16, EDGE>(g, grid, tp, s); break;
+    case 18: inv_int_go<18, EDGE>(g, grid, tp, s); break;
     default: break;
     }
 }
@@ -1645,31 +1611,32 @@ void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) 
             gi.dv_per = make_fastdiv((uint32_t)(nr * nc));
             gi.dv_ntc = make_fastdiv((uint32_t)nc);
             const int fr = g.geo.tilesR * g.geo.tilesC - nr * nc;
-            /* the frame's decode (k_fwd_int's edge form) */
-            gi.tiles_f = fr * B;
-            gi.dvf_tiles = make_fastdiv((uint32_t)std::max(1, gi.tiles_f));
-            gi.dvf_per = make_fastdiv((uint32_t)std::max(1, fr));
-            gi.dv_tc = make_fastdiv((uint32_t)g.geo.tilesC);
-            gi.dv_side = make_fastdiv((uint32_t)std::max(1, g.geo.tilesC - nc));
-            if (mode == 3 && fr > 0) {
-                /* the frame and the interior in ONE launch (round 5: the frame's own launch was as
-                 * long as the interior's at the small levels, and the two serialised) */
-                gi.nblk_f = gi.n * gi.tiles_f;
-                fwd_interior_go<FB_BOTH>(gi, gi.nblk_f + gi.n * gi.tiles, tp, s);
+            if (mode == 3 && fr > 0 && (int64_t)g.n * g.tiles <= FB_ONE_LAUNCH_TILES) {
+                /* a small level: every tile in ONE launch of the edge form (its decode with an empty
+                 * rectangle walks the whole grid row-major; interior tiles take its interior paths),
+                 * where the interior and the frame as two launches were latency cliffs (round 4: the
+                 * frame's launch as long as the interior's at levels 3-5) */
+                FwdGroup ga = g;
+                ga.geo.tr0 = 0; ga.geo.nTR = 0; ga.geo.tc0 = 0; ga.geo.nTC = 0;
+                ga.dv_tiles = make_fastdiv((uint32_t)ga.tiles);
+                ga.dv_per = make_fastdiv((uint32_t)ga.tiles / (uint32_t)B);
+                ga.dv_tc = make_fastdiv((uint32_t)g.geo.tilesC);
+                ga.dv_side = make_fastdiv((uint32_t)g.geo.tilesC);
+                fwd_interior_go<true>(ga, ga.n * ga.tiles, tp, s);
                 continue;
             }
-            fwd_interior_go<FB_INT>(gi, gi.n * gi.tiles, tp, s);
+            fwd_interior_go<false>(gi, gi.n * gi.tiles, tp, s);
             if (fr == 0) continue;
-            if (mode >= 2) {
-                fwd_interior_go<FB_FRAME>(gi, gi.n * gi.tiles_f, tp, s);
-                continue;
-            }
             g.geo.frame = 1;
             g.tiles = fr * B;
             g.dv_tiles = make_fastdiv((uint32_t)g.tiles);
             g.dv_per = make_fastdiv((uint32_t)fr);
             g.dv_tc = make_fastdiv((uint32_t)g.geo.tilesC);
             g.dv_side = make_fastdiv((uint32_t)std::max(1, g.geo.tilesC - nc));
+            if (mode >= 2) {
+                fwd_interior_go<true>(g, g.n * g.tiles, tp, s);
+                continue;
+            }
         }
         fwd_general(g, g.n * g.tiles, tp, s);
     }
@@ -1722,29 +1689,30 @@ void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s) 
             gi.dv_per = make_fastdiv((uint32_t)(nr * nc));
             gi.dv_ntc = make_fastdiv((uint32_t)nc);
             const int fr = g.geo.tilesR * g.geo.tilesC - nr * nc;
-            gi.tiles_f = fr * B;
-            gi.dvf_tiles = make_fastdiv((uint32_t)std::max(1, gi.tiles_f));
-            gi.dvf_per = make_fastdiv((uint32_t)std::max(1, fr));
-            gi.dv_tc = make_fastdiv((uint32_t)g.geo.tilesC);
-            gi.dv_side = make_fastdiv((uint32_t)std::max(1, g.geo.tilesC - nc));
             const bool edge_ok = inv_frame_ok(g.geo, tp.F);
-            if (mode == 3 && fr > 0 && edge_ok) { /* the frame and the interior in one launch (as the analysis) */
-                gi.nblk_f = gi.n * gi.tiles_f;
-                inv_interior_go<FB_BOTH>(gi, gi.nblk_f + gi.n * gi.tiles, tp, s);
+            if (mode == 3 && fr > 0 && edge_ok && (int64_t)g.n * g.tiles <= FB_ONE_LAUNCH_TILES) {
+                /* a small level: every tile in one launch of the edge form (as the analysis) */
+                InvGroup ga = g;
+                ga.geo.tr0 = 0; ga.geo.nTR = 0; ga.geo.tc0 = 0; ga.geo.nTC = 0;
+                ga.dv_tiles = make_fastdiv((uint32_t)ga.tiles);
+                ga.dv_per = make_fastdiv((uint32_t)ga.tiles / (uint32_t)B);
+                ga.dv_tc = make_fastdiv((uint32_t)g.geo.tilesC);
+                ga.dv_side = make_fastdiv((uint32_t)g.geo.tilesC);
+                inv_interior_go<true>(ga, ga.n * ga.tiles, tp, s);
                 continue;
             }
-            inv_interior_go<FB_INT>(gi, gi.n * gi.tiles, tp, s);
+            inv_interior_go<false>(gi, gi.n * gi.tiles, tp, s);
             if (fr == 0) continue;
-            if (mode >= 2 && edge_ok) {
-                inv_interior_go<FB_FRAME>(gi, gi.n * gi.tiles_f, tp, s);
-                continue;
-            }
             g.geo.frame = 1;
             g.tiles = fr * B;
             g.dv_tiles = make_fastdiv((uint32_t)g.tiles);
             g.dv_per = make_fastdiv((uint32_t)fr);
             g.dv_tc = make_fastdiv((uint32_t)g.geo.tilesC);
             g.dv_side = make_fastdiv((uint32_t)std::max(1, g.geo.tilesC - nc));
+            if (mode >= 2 && edge_ok) {
+                inv_interior_go<true>(g, g.n * g.tiles, tp, s);
+                continue;
+            }
         }
         inv_general(g, g.n * g.tiles, tp, s);
     }

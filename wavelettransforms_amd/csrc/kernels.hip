@@ -1273,43 +1273,11 @@ __device__ __forceinline__ uint32_t parity_late(uint32_t qv) {
     return q;
 }
 
-/* The decided float4s of a chunk -- every key outside the window [kl, kh] -- stored before the
- * threshold is known: a key below kl is below the threshold (kl <= ka <= thr32 when the window
- * holds both ranks) and becomes +0.0, a key above kh stays.  Only out of place (the segment's
- * input is intact for a full-scan fallback) and only as a first write: the last pass rewrites
- * every float4 when the window missed or the threshold is NaN, else the pending ones (pend). */
+/* k_resident's last pass: out = where(|x| < thr, 0, x) from registers; a NaN threshold prunes
+ * nothing and the copy's zeros are counted (the pad slots read as +0.0 excluded) */
 template <bool FULL>
-__device__ __forceinline__ void res_spec_store(const float4 (&v)[RES_IT], uint32_t pend, uint32_t kl, float* qo, int len,
-                                               bool al) {
-    constexpr int CT = RES_THREADS;
-    auto dec = [&](float xv) { return abs_key(xv) < kl ? 0.0f : xv; };
-    if (FULL) {
-        float4* q4 = reinterpret_cast<float4*>(qo);
-#pragma unroll
-        for (int it = 0; it < RES_IT; ++it) {
-            if ((pend >> it) & 1u) continue;
-            typedef float f4v __attribute__((ext_vector_type(4)));
-            const f4v yv = {dec(v[it].x), dec(v[it].y), dec(v[it].z), dec(v[it].w)};
-            __builtin_nontemporal_store(yv, reinterpret_cast<f4v*>(q4 + it * CT + threadIdx.x));
-        }
-    } else {
-        const __amdgpu_buffer_rsrc_t rr = ragged_rsrc(qo, len);
-#pragma unroll
-        for (int it = 0; it < RES_IT; ++it) {
-            if ((pend >> it) & 1u) continue;
-            const float4 y = make_float4(dec(v[it].x), dec(v[it].y), dec(v[it].z), dec(v[it].w));
-            store4_tail(y, qo, rr, it * CT + (int)threadIdx.x, len, al);
-        }
-    }
-}
-
-/* k_resident's last pass: out = where(|x| < thr, 0, x) from registers for the float4s in fmask
- * (every float4, or the pending ones where the decided ones went out ahead); a NaN threshold
- * prunes nothing and the copy's zeros are counted (the pad slots read as +0.0 excluded) */
-template <bool FULL>
-__device__ __forceinline__ void res_final(const float4 (&v)[RES_IT], uint32_t pend, float thr, uint32_t fmask,
-                                          const SegDesc& sd, wtp_result* __restrict__ res, int64_t base, int len,
-                                          bool al) {
+__device__ __forceinline__ void res_final(const float4 (&v)[RES_IT], float thr, const SegDesc& sd,
+                                          wtp_result* __restrict__ res, int64_t base, int len, bool al) {
     constexpr int CT = RES_THREADS, IT = RES_IT;
     const int tid = threadIdx.x;
     float* qo = sd.out + base;
@@ -1318,7 +1286,6 @@ __device__ __forceinline__ void res_final(const float4 (&v)[RES_IT], uint32_t pe
         float4* q4 = reinterpret_cast<float4*>(qo);
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            if (!((fmask >> it) & 1u)) continue;
             typedef float f4v __attribute__((ext_vector_type(4)));
             const f4v yv = {fin(v[it].x), fin(v[it].y), fin(v[it].z), fin(v[it].w)};
             __builtin_nontemporal_store(yv, reinterpret_cast<f4v*>(q4 + it * CT + tid));
@@ -1327,7 +1294,6 @@ __device__ __forceinline__ void res_final(const float4 (&v)[RES_IT], uint32_t pe
         const __amdgpu_buffer_rsrc_t rr = ragged_rsrc(qo, len);
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            if (!((fmask >> it) & 1u)) continue;
             const float4 y = make_float4(fin(v[it].x), fin(v[it].y), fin(v[it].z), fin(v[it].w));
             store4_tail(y, qo, rr, it * CT + tid, len, al);
         }
@@ -1462,7 +1428,6 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         sh = bits > RES_NSUB_LOG2 ? bits - RES_NSUB_LOG2 : 0;
     }
     uint32_t wbelow = 0, mx = 0, cnt = 0;
-    uint32_t pend = 0; /* bit it: float4 it holds a key inside [kl, kh] (its output waits for thr) */
     uint32_t* col = wstage + tid;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
@@ -1470,7 +1435,6 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
 #pragma unroll
         for (int c = 0; c < 4; ++c) k4[c] = abs_key(opaque(f4_get(v[it], c)));
         mx = max(mx, max(max(k4[0], k4[1]), max(k4[2], k4[3])));
-        uint32_t pin = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const uint32_t k = k4[c];
@@ -1478,12 +1442,8 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             wbelow += d >> 31;
             col[min(cnt, (uint32_t)RES_STG) * CT] = k;
             const bool valid = FULL || 4 * (it * CT + tid) + c < len;
-            const uint32_t in = d <= span;
-            pin |= in;
-            cnt += in & valid;
+            cnt += (d <= span) & valid;
         }
-        pend |= pin << it;
-        asm volatile("" : "+v"(pend)); /* kept as one word: left to itself the compiler keeps the 96 flags */
     }
     {
         wbelow = wave_sum_u32(wbelow);
@@ -1504,11 +1464,9 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     const uint32_t nwg = (uint32_t)((sd.n + RES_CHUNK - 1) / RES_CHUNK);
     const bool solo = nwg == 1u; /* block-uniform */
     /* remote: a shared segment whose select runs on its selector workgroup (a CU that holds no
-     * chunk, so the select's dependent round trips queue behind nobody's stores); its workgroups
-     * only wait for the threshold granule, and out of place they store their decided float4s
-     * (res_spec_store) while the selector works */
+     * chunk: the select's dependent round trips start from an idle memory queue); its workgroups
+     * only wait for the threshold granule */
     const bool remote = t.nsel > 0 && !solo; /* block-uniform */
-    const bool spec = remote && !sel && sd.out != sd.data && !ovf;
     const bool al = (sd.flags & SEG_ALIGNED) != 0;
     __shared__ unsigned long long s_cnt[1];
     __shared__ uint32_t s_mk, s_ovf;
@@ -1627,10 +1585,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         }
         if (tid == 0) s_ok1 = 1;
     } else if (wv == NW - 1 && remote && !sel) {
-        /* a remote segment's workgroup does not wait at barrier 1: wave 7 stores its decided
-         * float4s at once (the others after their publication) */
-        if (lane == 0) s_ok1 = 1;
-        if (spec) res_spec_store<FULL>(v, pend, kl, sd.out + base, len, al);
+        if (lane == 0) s_ok1 = 1; /* a remote segment's workgroup does not wait at barrier 1 */
     } else if (wv == NW - 1) {
         /* ---- barrier 1, polled by wave 7 while the others store (the selector: by wave 7) */
         if (lane == 0) {
@@ -1676,7 +1631,6 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);
             if (s_arr == nsh - 1u && atomicAdd(&bar->arrive[0][16], 1u) == nact - 1u) stc(&head->parity, q + 1u);
         }
-        if (spec) res_spec_store<FULL>(v, pend, kl, sd.out + base, len, al);
     }
     __syncthreads();
     WTP_RPROBE(11);
@@ -1693,7 +1647,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         /* ---- the threshold granule {thr bits, tag} from the segment's selector (one 8-byte sc1
          * word; the region is zero at the launch's start).  A wait that times out claims the
          * granule for FAULT by compare-and-swap, so every workgroup of the segment and the
-         * selector agree: all store, or none does (in place: nothing was stored yet) */
+         * selector agree: all store, or none does */
         __shared__ unsigned long long s_gr;
         if (wv == NW - 1 && lane == 0) {
             const uint64_t t0 = wall_ticks();
@@ -1720,8 +1674,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         }
         const float thr = __uint_as_float((uint32_t)g);
         WTP_RPROBE(6);
-        res_final<FULL>(v, pend, thr, (spec && !(tag & RES_GR_ALL) && thr == thr) ? pend : 0xFFFFFFFFu, sd, res, base,
-                        len, al);
+        res_final<FULL>(v, thr, sd, res, base, len, al);
         return;
     }
     /* ---- P2: the segment's counters and bucket totals in one round trip (every load in
@@ -1969,7 +1922,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     }
     WTP_RPROBE(6);
     /* ---- P3: out = where(|x| < thr, 0, x) from registers (a NaN threshold prunes nothing) */
-    res_final<FULL>(v, pend, thr, 0xFFFFFFFFu, sd, res, base, len, al);
+    res_final<FULL>(v, thr, sd, res, base, len, al);
     WTP_RPROBE(7);
 }
 

@@ -6,6 +6,7 @@ tensors on the current stream and returns the outputs plus the device-side resul
 numbers come from the HIP kernels, the host only packs pointers and decodes results.
 """
 import ctypes
+import warnings
 
 import numpy as np
 import torch
@@ -37,6 +38,12 @@ def workspace(device, nbytes, stream=None):
     key = (device.index, stream.cuda_stream)
     ws = _workspaces.get(key)
     if ws is None or ws.numel() < nbytes:
+        if torch.cuda.is_current_stream_capturing():
+            # the zero-fill below becomes a node of the graph and re-zeroes the workspace on every
+            # replay (correct, but a memset of the whole workspace per replay): warm the call up on
+            # the capturing stream first (torch.cuda.graph(g, stream=s) after a call on s)
+            warnings.warn("wavelettransforms_amd: workspace allocated inside a graph capture; its "
+                          "zero-fill is replayed with the graph", RuntimeWarning, stacklevel=3)
         # allocated (and zeroed) on the call's stream, so the caching allocator ties the block to it
         with torch.cuda.stream(stream):
             ws = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
@@ -231,10 +238,10 @@ def set_pipeline(enabled):
 
 
 def set_interior(enabled):
-    """Filter-bank kernel choice (include/wtprune.h wtp_set_interior): True / 3 the interior tiles
-    and the frame around them in the edge-free kernels and their edge form, one launch per level
-    (default), 2 the same as two launches, 1 the frame in the general kernel, False / 0 every tile
-    in the general kernel; returns the previous mode."""
+    """Filter-bank kernel choice (include/wtprune.h wtp_set_interior): 2 the interior tiles in the
+    edge-free kernels and the frame around them in their edge form, True / 3 the same but a small
+    level in one launch of the edge form (default), 1 the frame in the general kernel, False / 0
+    every tile in the general kernel; returns the previous mode."""
     mode = (3 if enabled else 0) if isinstance(enabled, bool) else int(enabled)
     return int(N.lib().wtp_set_interior(mode))
 
