@@ -138,6 +138,20 @@ int main(int argc, char** argv) {
         }
         printf("\n");
     }
+    {   /* the selector workgroups (past the chunks) of the last rep: when each passed barrier 1,
+         * read the totals, staged the keys and published the granule (us from the first start) */
+        int nb = 0; for (int t = 0; t < 20; ++t) { int64_t n = 1; for (int d = 0; d < 4; ++d) n *= shapes[t][d]; nb += (int)((n + RES_CHUNK - 1) / RES_CHUNK); }
+        unsigned long long t0 = ~0ull;
+        for (int i = 0; i < nb; ++i) t0 = std::min(t0, pr[i][0]);
+        static unsigned long long sp[NWG][16];
+        CK(hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_sprobe), sizeof sp));
+        auto us = [&](unsigned long long x) { return x >= t0 && x - t0 < 100000000ull ? (double)(x - t0) / 100.0 : -1.0; };
+        for (int i = nb; i < NWG; ++i) {
+            if (pr[i][0] < t0 || pr[i][0] - t0 > 100000000ull) continue;
+            printf("  selector %3d: start %6.2f  window %6.2f  B1-pass %6.2f  counters %6.2f  B2-pass %6.2f  staged %6.2f  ranks %6.2f  granule %6.2f\n",
+                   i, us(pr[i][0]), us(pr[i][1]), us(pr[i][5]), us(sp[i][1]), us(sp[i][4]), us(sp[i][5]), us(sp[i][6]), us(pr[i][6]));
+        }
+    }
     const char* snames[15] = {"-", "counters", "buckets", "B2-wait", "B2-pass", "staged", "ranks", "-", "-", "-", "-", "-", "-", "-", "-"};
     for (int p = 0; p < 15; ++p) {
         if (p == 0 || p >= 7) continue;

@@ -1870,6 +1870,16 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
     if (mk > 0x7F800000u) thr64 = __longlong_as_double(0x7FF8000000000000ll); /* NaN present: np.percentile is NaN */
     const float thr = (float)thr64;
     const bool nan = thr != thr; /* also inf - inf inside the lerp */
+    if (sel && tid == 0) {
+        /* the threshold granule for the segment's workgroups, ahead of the record: {thr bits, tag},
+         * claimed by compare-and-swap (a workgroup whose wait timed out may have claimed it for
+         * FAULT) */
+        const uint32_t tag = RES_GR_OK | (path == MODE_FULL ? RES_GR_ALL : 0u);
+        const unsigned long long gv = ((unsigned long long)tag << 32) | __float_as_uint(thr);
+        if (atomicCAS(reinterpret_cast<unsigned long long*>(gr), 0ull, gv) != 0ull)
+            atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
+    }
+    WTP_RPROBE(6);
     if (first || sel) {
         /* zeros of where(|x| < thr, 0, x) = #(key < tk), tk = bits(thr) when thr > 0, else 1 (only
          * the zeros themselves); ka <= thr <= kb and the ranks are adjacent, so #(key < tk) =
@@ -1902,17 +1912,7 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
             atomicMax(&r.path, path);
         }
     }
-    if (sel) {
-        /* the threshold granule for the segment's workgroups: {thr bits, tag}, claimed by
-         * compare-and-swap (a workgroup whose wait timed out may have claimed it for FAULT) */
-        if (tid == 0) {
-            const uint32_t tag = RES_GR_OK | (path == MODE_FULL ? RES_GR_ALL : 0u);
-            const unsigned long long gv = ((unsigned long long)tag << 32) | __float_as_uint(thr);
-            if (atomicCAS(reinterpret_cast<unsigned long long*>(gr), 0ull, gv) != 0ull)
-                atomicMax(&res[sd.res].path, (int32_t)MODE_FAULT);
-        }
-        return;
-    }
+    if (sel) return;
     if (path == MODE_FULL && sd.out == sd.data) { /* in place: nobody writes before the segment's scans end */
         res_arrive(b0);
         if (!res_wait(b0, nwg, tmo)) {
