@@ -17,7 +17,7 @@ echo "== bench cfg2"; timeout -k 10 300 python bench.py > "$OUT/bench_cfg2_$TAG.
 tail -1 "$OUT/bench_cfg2_$TAG.log"
 echo "== bench cfg3"; timeout -k 10 300 python bench.py --config cfg3 > "$OUT/bench_cfg3_$TAG.log" 2>&1 || { echo bench cfg3 failed; tail -30 "$OUT/bench_cfg3_$TAG.log"; exit 1; }
 tail -1 "$OUT/bench_cfg3_$TAG.log" | cut -c1-600
-echo "== bench cfg5"; timeout -k 10 400 python bench.py --config cfg5 --steps 20 --warmup 3 > "$OUT/bench_cfg5_$TAG.log" 2>&1 || { echo bench cfg5 failed; tail -30 "$OUT/bench_cfg5_$TAG.log"; exit 1; }
+echo "== bench cfg5"; WTP_BENCH_TRACE_DIR="$OUT/trace5_$TAG" timeout -k 10 400 python bench.py --config cfg5 --steps 20 --warmup 3 > "$OUT/bench_cfg5_$TAG.log" 2>&1 || { echo bench cfg5 failed; tail -30 "$OUT/bench_cfg5_$TAG.log"; exit 1; }
 tail -1 "$OUT/bench_cfg5_$TAG.log" | cut -c1-600
 echo "== rehearsal --gpus 2"; WTP_BENCH_REHEARSAL=1 timeout -k 10 300 python bench.py --gpus 2 --steps 40 --warmup 5 > "$OUT/bench_n2_$TAG.log" 2>&1 || { echo rehearsal failed; tail -30 "$OUT/bench_n2_$TAG.log"; exit 1; }
 grep '"metric"' "$OUT/bench_n2_$TAG.log" | cut -c1-400
@@ -29,4 +29,6 @@ echo "== pmc cfg2"; cd "$ROOT" && timeout -k 10 600 bash tools/pmc_run.sh "$TAG"
 python3 tools/pmc_summary.py "$OUT/pmc_$TAG" "$OUT/pmc_${TAG}_cfg2.json" "$TAG" || exit 1
 echo "== pmc cfg3"; timeout -k 10 600 bash tools/pmc_run.sh "${TAG}c3" --config cfg3 > "$OUT/pmc_${TAG}c3.log" 2>&1 || { echo pmc cfg3 failed; tail -20 "$OUT/pmc_${TAG}c3.log"; exit 1; }
 python3 tools/pmc_summary.py "$OUT/pmc_${TAG}c3" "$OUT/pmc_${TAG}_cfg3.json" "${TAG}c3" || exit 1
+echo "== pmc cfg5"; timeout -k 10 900 bash tools/pmc_run.sh "${TAG}c5" --config cfg5 --steps 3 --warmup 1 > "$OUT/pmc_${TAG}c5.log" 2>&1 || { echo pmc cfg5 failed; tail -20 "$OUT/pmc_${TAG}c5.log"; exit 1; }
+python3 tools/pmc_summary.py "$OUT/pmc_${TAG}c5" "$OUT/pmc_${TAG}_cfg5.json" "${TAG}c5" || exit 1
 echo done
