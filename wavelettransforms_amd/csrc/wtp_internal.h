@@ -196,8 +196,10 @@ constexpr int RES_SIGMA_X100 = 400;
 constexpr int RES_MAX_WG = 256;                     /* workgroups a resident launch may hold (<= CUs) */
 /* the late group: the smallest segments of a launch group, together at most this percentage of
  * its workgroups; their workgroups issue their chunk's loads only once their window is known, so
- * the early group's chunks come off HBM first and its select overlaps the late group's stream */
-constexpr int RES_LATE_PCT = 45;
+ * the early group's chunks come off HBM first and its select overlaps the late group's stream
+ * (round 5, with selector workgroups, cfg2: 0 / 25 / 45 / 60 / 80 / 99 % -> 28.1 / 27.8 / 26.1 /
+ * 25.85 / 27.6 / 27.8 us, A/B on one box; 60 % puts one of the three 48-workgroup layers late) */
+constexpr int RES_LATE_PCT = 60;
 constexpr int RES_STG = 32;                         /* inside keys a thread may stage (of its 96; ~11 expected) */
 /* After the first segment barrier every workgroup publishes the keys of the (one or two)
  * buckets holding the segment's ranks in a slot of its own: word 0 the count, then the keys */
