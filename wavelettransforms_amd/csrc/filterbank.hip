@@ -661,6 +661,17 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
     __syncthreads();
     WTP_FPROBE(2);
     /* 3. axis -1 of the L and H rows -> aa, ad, da, dd; two rows per step, four sums interleaved */
+    constexpr int NW = FB_THREADS / 64, NPR = FR / (2 * NW);
+    static_assert(FR % (2 * NW) == 0, "row pairs per wave");
+    auto flo = [&](int k) { return (k & 1) ? tp.t[k >> 1].y : tp.t[k >> 1].x; };
+    /* EDGE: the outputs whose site wraps past the row's end (ic >= C: the level's last F/4 or so
+     * columns) are skipped by the uniform pass and computed in wt_ana_point's split order by a
+     * compact fix-up: lane e of the wave = (its row e / nsc, the (e % nsc)-th such column) */
+    uint64_t fxm = 0;
+    if constexpr (EDGE) {
+        const int ic = FT / 2 + 2 * (o0c + lane);
+        fxm = __ballot(lane < FC && ic >= a.C && o0c + lane < a.Co);
+    }
     if (lane < FC) {
         const __amdgpu_buffer_rsrc_t rP =
             __builtin_amdgcn_make_buffer_rsrc(g.P[item] + (int64_t)b * a.P_bs, 0, (int)(4 * a.P_bs), 0x00020000);
@@ -668,14 +679,10 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
             : __builtin_amdgcn_make_buffer_rsrc(g.anext[item] + (int64_t)b * a.Ro * a.Co, 0, 4 * a.Ro * a.Co, 0x00020000);
         const int pitchA = a.last ? a.PC : a.Co;
         const int voff = 4 * (o0c + lane);
-        auto flo = [&](int k) { return (k & 1) ? tp.t[k >> 1].y : tp.t[k >> 1].x; };
         const int ic = FT / 2 + 2 * (o0c + lane); /* the lane's output site along the row */
-        const bool cedge = EDGE && !__all(ic < a.C);
-        const bool cin = !EDGE || o0c + lane < a.Co;
-        constexpr int NW = FB_THREADS / 64;
-        static_assert(FR % (2 * NW) == 0, "row pairs per wave");
+        const bool cin = !EDGE || (o0c + lane < a.Co && ic < a.C);
 #pragma unroll
-        for (int pr = 0; pr < FR / (2 * NW); ++pr) {
+        for (int pr = 0; pr < NPR; ++pr) {
             const int oA = wv + 2 * NW * pr, oB = oA + NW;
             f2 vA[FT], vB[FT];
 #pragma unroll
@@ -686,34 +693,17 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
             }
             const f2 z2 = {0.0f, 0.0f};
             f2 aA, dA, aB, dB;
-            if (!cedge) {
-                aA = z2 + flo(0) * vA[0];
-                dA = z2 + flo(1) * vA[0];
-                aB = z2 + flo(0) * vB[0];
-                dB = z2 + flo(1) * vB[0];
+            aA = z2 + flo(0) * vA[0];
+            dA = z2 + flo(1) * vA[0];
+            aB = z2 + flo(0) * vB[0];
+            dB = z2 + flo(1) * vB[0];
 #pragma unroll
-                for (int j = 1; j < FT; ++j) {
-                    const float tl = flo(2 * j), th = flo(2 * j + 1);
-                    aA = aA + tl * vA[j];
-                    dA = dA + th * vA[j];
-                    aB = aB + tl * vB[j];
-                    dB = dB + th * vB[j];
-                }
-            } else { /* wt_ana_point's split order where ic >= N, as the column pass */
-                aA = z2; dA = z2; aB = z2; dB = z2;
-                auto term = [&](int j) {
-                    const float tl = flo(2 * j), th = flo(2 * j + 1);
-                    aA = aA + tl * vA[j];
-                    dA = dA + th * vA[j];
-                    aB = aB + tl * vB[j];
-                    dB = dB + th * vB[j];
-                };
-#pragma unroll
-                for (int j = FT - 1; j >= 0; --j)
-                    if (ic - j >= a.C) term(j);
-#pragma unroll
-                for (int j = 0; j < FT; ++j)
-                    if (ic - j < a.C) term(j);
+            for (int j = 1; j < FT; ++j) {
+                const float tl = flo(2 * j), th = flo(2 * j + 1);
+                aA = aA + tl * vA[j];
+                dA = dA + th * vA[j];
+                aB = aB + tl * vB[j];
+                dB = dB + th * vB[j];
             }
             /* low = (aa, da), high = (ad, dd) */
 #pragma unroll
@@ -725,6 +715,42 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.x), rP, voff, 4 * (r * a.PC + a.offC), 0);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.y), rP, voff, 4 * ((a.offR + r) * a.PC), 0);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.y), rP, voff, 4 * ((a.offR + r) * a.PC + a.offC), 0);
+            }
+        }
+    }
+    if (EDGE && fxm) { /* uniform */
+        const int nsc = __builtin_popcountll(fxm);
+        static_assert(2 * NPR * (FT / 4 + 2) <= 64, "one fix-up pass per wave");
+        if (lane < 2 * NPR * nsc) {
+            const int rs = lane / nsc, ci = lane - rs * nsc;
+            uint64_t mm = fxm;
+            for (int t = 0; t < ci; ++t) mm &= mm - 1ull;
+            const int cl = __builtin_ctzll(mm); /* the column's lane in the uniform pass */
+            const int o = wv + NW * rs;       /* the wave's rows: wv + NW * (2 pr + u) */
+            const int r = o0r + o;
+            if (r < a.Ro) {
+                const int ic = FT / 2 + 2 * (o0c + cl);
+                f2 v[FT];
+#pragma unroll
+                for (int j = 0; j < FT; ++j) { const float2 xv = LH[lhi(o, 2 * cl + FT - 1 - j)]; v[j] = f2{xv.x, xv.y}; }
+                f2 lw = {0.0f, 0.0f}, hg = {0.0f, 0.0f};
+                auto term = [&](int j) { lw = lw + flo(2 * j) * v[j]; hg = hg + flo(2 * j + 1) * v[j]; };
+#pragma unroll
+                for (int j = FT - 1; j >= 0; --j)
+                    if (ic - j >= a.C) term(j);
+#pragma unroll
+                for (int j = 0; j < FT; ++j)
+                    if (ic - j < a.C) term(j);
+                const __amdgpu_buffer_rsrc_t rP =
+                    __builtin_amdgcn_make_buffer_rsrc(g.P[item] + (int64_t)b * a.P_bs, 0, (int)(4 * a.P_bs), 0x00020000);
+                const __amdgpu_buffer_rsrc_t rA = a.last ? rP
+                    : __builtin_amdgcn_make_buffer_rsrc(g.anext[item] + (int64_t)b * a.Ro * a.Co, 0, 4 * a.Ro * a.Co, 0x00020000);
+                const int pitchA = a.last ? a.PC : a.Co;
+                const int vo = 4 * (o0c + cl);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.x), rA, vo, 4 * r * pitchA, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.x), rP, vo, 4 * (r * a.PC + a.offC), 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.y), rP, vo, 4 * ((a.offR + r) * a.PC), 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.y), rP, vo, 4 * ((a.offR + r) * a.PC + a.offC), 0);
             }
         }
     }
@@ -1141,36 +1167,73 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
     const int m = m0 + lane;
     constexpr int KP = (NR + 7) / 8; /* row pairs per wave */
     f2 rowres[KP][2];
+    /* EDGE: the exact-order results of this lane's fix-up entry (row fxrow, column pair fxc) */
+    f2 fx[2] = {f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};
+    int fxrow = -1, fxc = 0;
     {
         const int ro = lane >> 5, c = lane & 31;
         /* both sub-passes from one sample window: p's samples start at column c + pe(p), and the
          * two sums are independent chains that interleave */
         constexpr int PE1 = (H & 1) ? 0 : 1, NS = HM + PE1;
         constexpr int PAR0 = (H & 1) ? 0 : 1, PAR1 = 1 - PAR0;
-        /* EDGE: the sites of the lane's two outputs and their order rule -- wt_syn_pass adds the
-         * terms with i - j >= T by descending j first (T = 0 at a special site, N past the end),
-         * then the others ascending; an interior site (i < N, T = N) has no first-loop term */
-        int i0 = 0, i1 = 0, T0 = 0, T1 = 0;
-        bool redge = false;
+        /* the two outputs of column pair cp at (unwrapped) sample row pa / pd in wt_syn_pass's
+         * order: the terms with i - j >= T by descending j first (T = 0 at a special site, N past
+         * the end), then the others ascending */
+        auto exact_pair = [&](const float2* pa, const float2* pd, int cp, f2& a0, f2& a1) {
+            const SiteU s0 = site_u(m0 + 2 * cp, a.C, FT), s1 = site_u(m0 + 2 * cp + 1, a.C, FT);
+            const int i0 = s0.i, T0 = s0.special ? 0 : a.C, i1 = s1.i, T1 = s1.special ? 0 : a.C;
+            f2 v[NS];
+            auto sp = [&](int p, int j) { return v[(p ? PE1 : 0) + HM - 1 - j]; };
+            a0 = f2{0.0f, 0.0f};
+            a1 = f2{0.0f, 0.0f};
+            auto pass = [&](const float* rec) {
+#pragma unroll
+                for (int j = HM - 1; j >= 0; --j) {
+                    if (i0 - j >= T0) a0 = a0 + rec[2 * j + PAR0] * sp(0, j);
+                    if (i1 - j >= T1) a1 = a1 + rec[2 * j + PAR1] * sp(1, j);
+                }
+#pragma unroll
+                for (int j = 0; j < HM; ++j) {
+                    if (i0 - j < T0) a0 = a0 + rec[2 * j + PAR0] * sp(0, j);
+                    if (i1 - j < T1) a1 = a1 + rec[2 * j + PAR1] * sp(1, j);
+                }
+            };
+#pragma unroll
+            for (int q = 0; q < NS; ++q) { const float2 t = pa[q]; v[q] = f2{t.x, t.y}; }
+            pass(tp.f[2]);
+#pragma unroll
+            for (int q = 0; q < NS; ++q) { const float2 t = pd[q]; v[q] = f2{t.x, t.y}; }
+            pass(tp.f[3]);
+        };
+        /* EDGE: the column pairs whose sites are special or past the end get the exact order in
+         * a compact fix-up after the uniform pass: lane e of this wave = (its row e / nsc, the
+         * (e % nsc)-th such pair).  Such pairs within the stored extent are the first one (H
+         * even: output 0) or the last F/4 + 1 of the level, never both in one tile (the host runs
+         * the frame only when the level is >= NC coefficients wide, so 2N > IC): at most F/4 + 1
+         * pairs, and the wave's 2 KP rows times that fit its 64 lanes. */
+        static_assert(2 * KP * (FT / 4 + 1) <= 64, "one fix-up pass per wave");
+        uint32_t fxmask = 0;
+        int nsc = 0;
         if constexpr (EDGE) {
             const SiteU s0 = site_u(m0 + 2 * c, a.C, FT), s1 = site_u(m0 + 2 * c + 1, a.C, FT);
-            i0 = s0.i; T0 = s0.special ? 0 : a.C;
-            i1 = s1.i; T1 = s1.special ? 0 : a.C;
-            redge = __any(s0.special || s0.i >= a.C || s1.special || s1.i >= a.C);
+            /* pairs past the stored extent (a partial last tile) are never read: left out */
+            const bool need = (s0.special || s0.i >= a.C || s1.special || s1.i >= a.C) && m0 + 2 * c <= ml;
+            fxmask = (uint32_t)__ballot(need && ro == 0); /* lanes 0..31: bit c */
+            nsc = __builtin_popcount(fxmask);
         }
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
             const int row = min(2 * (wv + 4 * k) + ro, NR - 1);
             const float2* pa = Aq + row * NC + c;
             const float2* pd = Dq + row * NC + c;
-            f2 v[NS];
-            /* sample of sub-pass p at tap j: column c + pe(p) + HM - 1 - j */
-            auto sp = [&](int p, int j) { return v[(p ? PE1 : 0) + HM - 1 - j]; };
-#pragma unroll
-            for (int q = 0; q < NS; ++q) { const float2 t = pa[q]; v[q] = f2{t.x, t.y}; }
-            const f2 z2 = {0.0f, 0.0f};
             f2 a0, a1;
-            if (!redge) {
+            {
+                f2 v[NS];
+                /* sample of sub-pass p at tap j: column c + pe(p) + HM - 1 - j */
+                auto sp = [&](int p, int j) { return v[(p ? PE1 : 0) + HM - 1 - j]; };
+#pragma unroll
+                for (int q = 0; q < NS; ++q) { const float2 t = pa[q]; v[q] = f2{t.x, t.y}; }
+                const f2 z2 = {0.0f, 0.0f};
                 a0 = z2 + tp.f[2][PAR0] * sp(0, 0);
                 a1 = z2 + tp.f[2][PAR1] * sp(1, 0);
 #pragma unroll
@@ -1185,31 +1248,30 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
                     a0 = a0 + tp.f[3][2 * j + PAR0] * sp(0, j);
                     a1 = a1 + tp.f[3][2 * j + PAR1] * sp(1, j);
                 }
-            } else {
-                a0 = z2;
-                a1 = z2;
-                auto pass = [&](const float* rec) {
-#pragma unroll
-                    for (int j = HM - 1; j >= 0; --j) {
-                        if (i0 - j >= T0) a0 = a0 + rec[2 * j + PAR0] * sp(0, j);
-                        if (i1 - j >= T1) a1 = a1 + rec[2 * j + PAR1] * sp(1, j);
-                    }
-#pragma unroll
-                    for (int j = 0; j < HM; ++j) {
-                        if (i0 - j < T0) a0 = a0 + rec[2 * j + PAR0] * sp(0, j);
-                        if (i1 - j < T1) a1 = a1 + rec[2 * j + PAR1] * sp(1, j);
-                    }
-                };
-                pass(tp.f[2]);
-#pragma unroll
-                for (int q = 0; q < NS; ++q) { const float2 t = pd[q]; v[q] = f2{t.x, t.y}; }
-                pass(tp.f[3]);
             }
             /* computed HERE: without this the compiler sinks the sums past the barrier below
              * (their only use is the LoHi write) and keeps every sample alive across it */
             asm volatile("" : "+v"(a0), "+v"(a1));
             rowres[k][0] = a0;
             rowres[k][1] = a1;
+        }
+        if (EDGE && fxmask) { /* uniform */
+            if (lane < 2 * KP * nsc) {
+                const int rs = lane / nsc, ci = lane - rs * nsc;
+                uint32_t mm = fxmask;
+                for (int t = 0; t < ci; ++t) mm &= mm - 1u;
+                const int cp = __builtin_ctz(mm);
+                const int row = 2 * (wv + 4 * (rs >> 1)) + (rs & 1);
+                if (row < NR) {
+                    f2 a0, a1;
+                    exact_pair(Aq + row * NC + cp, Dq + row * NC + cp, cp, a0, a1);
+                    asm volatile("" : "+v"(a0), "+v"(a1));
+                    fx[0] = a0;
+                    fx[1] = a1;
+                    fxrow = row;
+                    fxc = cp;
+                }
+            }
         }
     }
     __syncthreads(); /* every read of Aq/Dq is done: LoHi overwrites them */
@@ -1222,6 +1284,12 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
 #pragma unroll
                 for (int p = 0; p < 2; ++p) LoHi[row * IC + 2 * c + p] = make_float2(rowres[k][p].x, rowres[k][p].y);
             }
+        }
+        /* the fix-up's exact values over the uniform pass's (this wave's own rows; a wave's LDS
+         * writes land in program order) */
+        if (EDGE && fxrow >= 0) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p) LoHi[fxrow * IC + 2 * fxc + p] = make_float2(fx[p].x, fx[p].y);
         }
     }
     __syncthreads();
@@ -1240,40 +1308,20 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
         __builtin_amdgcn_make_buffer_rsrc(g.y[item] + (int64_t)b * a.outH * a.outW, 0, 4 * a.outH * a.outW, 0x00020000);
     const int vy = 4 * m;
     uint32_t z = 0; /* wave-uniform: zeros of this wave's outputs */
-    bool cedge = false;
+    /* EDGE: rows whose site is special or wrapped (the image's first / last few) are computed
+     * again one by one in wt_syn_pass's order after the packed pass, which skips storing them;
+     * rows past the extent are not stored.  The row's site is wave-uniform, so are the masks. */
+    uint32_t xmask = 0, smask = (1u << RB) - 1u;
     if constexpr (EDGE) {
-        /* a block holding a special or wrapped site (or outputs past the extent) runs its rows one
-         * by one in wt_syn_pass's order; the row's site is wave-uniform, so are the branches */
         for (int k = 0; k < RB; ++k) {
             const SiteU s = site_u(nf + k, a.R, FT);
-            cedge |= s.special || s.i >= a.R || nf + k > nl;
+            if (s.special || s.i >= a.R) xmask |= 1u << k;
+            if (nf + k > nl) smask &= ~(1u << k);
         }
     }
-    if (cedge) {
-        const bool min_ = m <= ml;
-#pragma unroll
-        for (int k = 0; k < RB; ++k) {
-            const int n = nf + k;
-            const SiteU s = site_u(n, a.R, FT);
-            const int Tn = s.special ? 0 : a.R;
-            const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
-            float y = 0.0f;
-#pragma unroll
-            for (int pass = 0; pass < 2; ++pass) {
-                const float* rec = tp.f[2 + pass];
-#pragma unroll
-                for (int j = H - 1; j >= 0; --j)
-                    if (s.i - j >= Tn) y = y + rec[2 * j + par] * (pass ? r[base - j].y : r[base - j].x);
-#pragma unroll
-                for (int j = 0; j < H; ++j)
-                    if (s.i - j < Tn) y = y + rec[2 * j + par] * (pass ? r[base - j].y : r[base - j].x);
-            }
-            if (n <= nl) {
-                if (min_) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), rY, vy, 4 * n * a.outW, 0);
-                z += (uint32_t)__popcll(__ballot(min_ && y == 0.0f));
-            }
-        }
-    } else {
+    const bool min_ = !EDGE || m <= ml; /* EDGE: a partial last tile column */
+    {
+        const uint32_t wmask = smask & ~xmask; /* the rows the packed pass stores */
         f2 acc[RB2];
 #pragma unroll
         for (int j = 0; j < H; ++j) {
@@ -1296,14 +1344,49 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_inv_int(InvGroup 
                 acc[k] = acc[k] + f2{t, t} * f2{r[base - j].y, r[base - j + RB2 / 2].y};
             }
         }
-        const bool min_ = !EDGE || m <= ml; /* EDGE: a partial last tile column */
+        if constexpr (!EDGE) {
 #pragma unroll
-        for (int k = 0; k < RB2; ++k) {
-            if (min_) {
+            for (int k = 0; k < RB2; ++k) {
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[k].x), rY, vy, 4 * (nf + k) * a.outW, 0);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[k].y), rY, vy, 4 * (nf + k + RB2) * a.outW, 0);
+                z += (uint32_t)__popcll(__ballot(acc[k].x == 0.0f)) + (uint32_t)__popcll(__ballot(acc[k].y == 0.0f));
             }
-            z += (uint32_t)__popcll(__ballot(min_ && acc[k].x == 0.0f)) + (uint32_t)__popcll(__ballot(min_ && acc[k].y == 0.0f));
+        } else {
+#pragma unroll
+            for (int k = 0; k < RB2; ++k) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int kk = k + u * RB2;
+                    const float y = u ? acc[k].y : acc[k].x;
+                    if ((wmask >> kk) & 1u) {
+                        if (min_) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), rY, vy, 4 * (nf + kk) * a.outW, 0);
+                        z += (uint32_t)__popcll(__ballot(min_ && y == 0.0f));
+                    }
+                }
+            }
+        }
+    }
+    if (EDGE && (xmask & smask)) { /* uniform */
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            if (!(((xmask & smask) >> k) & 1u)) continue;
+            const int n = nf + k;
+            const SiteU s = site_u(n, a.R, FT);
+            const int Tn = s.special ? 0 : a.R;
+            const int par = (k + E) & 1, base = ((k + E) >> 1) + H - 1;
+            float y = 0.0f;
+#pragma unroll
+            for (int pass = 0; pass < 2; ++pass) {
+                const float* rec = tp.f[2 + pass];
+#pragma unroll
+                for (int j = H - 1; j >= 0; --j)
+                    if (s.i - j >= Tn) y = y + rec[2 * j + par] * (pass ? r[base - j].y : r[base - j].x);
+#pragma unroll
+                for (int j = 0; j < H; ++j)
+                    if (s.i - j < Tn) y = y + rec[2 * j + par] * (pass ? r[base - j].y : r[base - j].x);
+            }
+            if (min_) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), rY, vy, 4 * n * a.outW, 0);
+            z += (uint32_t)__popcll(__ballot(min_ && y == 0.0f));
         }
     }
     if (a.zc) {
