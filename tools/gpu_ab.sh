@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B on one box: parity of the changed paths, then each config's bench line with the
 # working tree's library ("new") and tools/ab/libwtprune_base.so ("base", tools/build_base.sh),
-# alternated twice; the k_resident phase lab last.
+# alternated twice; the k_resident phase lab last.  NEW_LIB / BASE_LIB override either library
+# (e.g. a lab build under tools/ab/); PARITY="" skips the parity step.
 # Usage: gpurun --timeout 1100 -- bash tools/gpu_ab.sh TAG [configs]
 set -o pipefail
 TAG=${1:-ab}
@@ -10,14 +11,16 @@ cd ${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
-echo "== parity"
-PARITY=${PARITY:-tests/test_gpu_resident.py tests/test_gpu_small.py tests/test_gpu_large_levels.py tests/test_gpu_parity.py tests/test_gpu_pipeline.py tests/test_gpu_cfg5_bench_call.py}
-timeout -k 10 700 python -u -m pytest $PARITY -x -q --timeout 300 --timeout-method thread > $OUT/par_$TAG.log 2>&1 || { echo parity failed; grep -E "FAIL|Error|assert" $OUT/par_$TAG.log | head -30; tail -30 $OUT/par_$TAG.log; exit 1; }
-tail -1 $OUT/par_$TAG.log
+PARITY=${PARITY-tests/test_gpu_resident.py tests/test_gpu_small.py tests/test_gpu_large_levels.py tests/test_gpu_parity.py tests/test_gpu_pipeline.py tests/test_gpu_cfg5_bench_call.py}
+if [ -n "$PARITY" ]; then
+  echo "== parity"
+  timeout -k 10 700 python -u -m pytest $PARITY -x -q --timeout 300 --timeout-method thread > $OUT/par_$TAG.log 2>&1 || { echo parity failed; grep -E "FAIL|Error|assert" $OUT/par_$TAG.log | head -30; tail -30 $OUT/par_$TAG.log; exit 1; }
+  tail -1 $OUT/par_$TAG.log
+fi
 for c in $CFGS; do
   X=""; [ $c = cfg5 ] && X="--steps 10 --warmup 2 --replays 10"
   for v in new base new base; do
-    L=""; [ $v = base ] && L=$(pwd)/tools/ab/libwtprune_base.so
+    L=${NEW_LIB:-}; [ $v = base ] && L=${BASE_LIB:-$(pwd)/tools/ab/libwtprune_base.so}
     WTP_LIB_PATH=$L timeout -k 10 300 python bench.py --config $c --no-cpu --no-cold $X > $OUT/b_${TAG}_${c}_$v.log 2>&1 || { tail -20 $OUT/b_${TAG}_${c}_$v.log; exit 1; }
     python3 -c "
 import json
