@@ -51,8 +51,11 @@ def test_interior_kernels_equal_general(wavelet):
     form), and in the general kernels (mode 1), against every tile
     in the general kernels (mode 0): packed coefficients and pruned outputs bit for bit, on shapes
     with an interior and a frame (odd extents, batches, partial last tiles, a 2-level and a 4-level
-    tree; the deepest levels of the narrow shape fall back to the general frame)."""
-    shapes = [(1, 2, 700, 1100), (1, 1, 1031, 515), (800, 1600), (2, 1, 333, 4100)]
+    tree; the deepest levels of the narrow shape fall back to the general frame; levels of 40-48
+    coefficients, just wide enough for the EDGE frame, where a tile holds the level's last
+    special / wrapped sites behind a partial extent -- the fix-up passes' densest case)."""
+    shapes = [(1, 2, 700, 1100), (1, 1, 1031, 515), (800, 1600), (2, 1, 333, 4100), (1, 1, 170, 180),
+              (1, 1, 680, 700)]
     prev = eng.set_interior(3)
     try:
         for j, shp in enumerate(shapes):
