@@ -61,7 +61,8 @@ def parse():
     ap.add_argument("--graph-steps", type=int, default=10, help="steps captured per hipGraph replay")
     ap.add_argument("--replays", type=int, default=60, help="graph replays timed one by one (p10/p50/p90)")
     ap.add_argument("--stamp-reps", type=int, default=50, help="launches timed by in-kernel stamps")
-    ap.add_argument("--stage-reps", type=int, default=20)
+    ap.add_argument("--stage-reps", type=int, default=20,
+                    help="calls timed stage by stage (0: no stage leg and no roofline object; tools/pmc_run.sh)")
     ap.add_argument("--cold-reps", type=int, default=30)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -466,7 +467,7 @@ def main():
         timing_src = ("in-kernel s_memrealtime stamps: first workgroup start -> last workgroup end after its "
                       "stores completed, mean of %d back-to-back launches (wtp_set_kernel_stamps)" % len(spans))
         stage_us = {dom: dom_us}
-    elif xs:
+    elif xs and args.stage_reps > 0:
         # stage intervals from HIP events the library records between its launches (include dispatch
         # gaps); a spin kernel in front lets the whole call be enqueued before it runs
         sevs = [torch.cuda.Event(enable_timing=True) for _ in range(len(STAGES) + 1)]
