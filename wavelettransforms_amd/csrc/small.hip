@@ -538,9 +538,6 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
         if (atomicAdd(&br->arrive[sh][0], 1u) == nsh - 1u && atomicAdd(&br->arrive[0][16], 1u) == nact - 1u)
             sm_stc(&head->parity, q + 1u);
     }
-    bool ok = sm_wait(&st->bar[0][0], a0, nwg, tmo, &s_ok);
-    SM_PROBE(11);
-
     /* inverse arena: [owned keys | coefficient windows of levels 1..L | synthesised cA | row-pass
      * rows | tap tables]; level k's windows: cV (ad), cH (da), cD (dd) planes, and cA at level L */
     float* WIN = reinterpret_cast<float*>(K) + sm_r4(nkeys);
@@ -563,6 +560,18 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
         const int cc = pl == 0 || pl == 2 ? g.offC[k] + c : c;
         return P + (int64_t)rr * g.PC + cc;
     };
+
+    /* this thread's prefetch words of the windows (see barrier 1), as element offsets from P: their
+     * address arithmetic (a level search and two divisions a word) done while barrier 0 is awaited
+     * -- done behind barrier 1's arrival it delayed that barrier's poll by ~1.5 us */
+    uint32_t woff[SM_PF];
+#pragma unroll
+    for (int u = 0; u < SM_PF; ++u) {
+        const int e = tid + u * SM_THREADS;
+        woff[u] = e < nwin ? (uint32_t)(win_src(e) - P) : 0u;
+    }
+    bool ok = sm_wait(&st->bar[0][0], a0, nwg, tmo, &s_ok);
+    SM_PROBE(11);
 
     /* ---------------- S: the two order statistics ---------------- */
     /* locate ranks ra <= rb in nb bins (get(i): count of bin i, every load of a thread issued
@@ -636,7 +645,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
 #pragma unroll
         for (int u = 0; u < SM_PF; ++u) {
             const int e = tid + u * SM_THREADS;
-            pv[u] = e < nwin ? sm_ldc(win_src(e)) : 0.0f;
+            pv[u] = e < nwin ? sm_ldc(P + woff[u]) : 0.0f;
         }
         ok = sm_wait(&st->bar[1][0], a1, nwg, tmo, &s_ok);
         SM_PROBE(5);
