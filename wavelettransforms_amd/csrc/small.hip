@@ -301,6 +301,11 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     __shared__ int s_ok, s_dig[2];
     __shared__ uint32_t s_bef[2];
     __shared__ float staps[4][SM_F_MAX]; /* dec_lo, dec_hi, rec_lo, rec_hi */
+    /* the inverse windows' per-level constants, for the window-word -> packed-offset map (win_src):
+     * built once from the axes and the segment geometry, read from LDS at every word instead of
+     * the kernel argument's per-level arrays indexed by a per-lane level */
+    struct WinLvl { int base, ns, scl, srs, scs, R, C, offR, offC; float rns, rsc; int pad; };
+    __shared__ WinLvl s_wl[SM_LMAX + 2];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t q = head->parity;
     if (t.stamps && tid == 0) atomicMin(t.stamps, sm_ticks()); /* measurement only */
@@ -355,6 +360,28 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     __syncthreads();
     SM_PROBE(0);
 
+    if (tid == 0) {
+        int base = 0;
+        for (int k = 1; k <= L + 1; ++k) {
+            WinLvl w{};
+            w.base = base;
+            if (k <= L) {
+                const SmIvl sr = axr.sv[k], sc = axc.sv[k];
+                w.ns = sr.len * sc.len;
+                w.scl = sc.len;
+                w.srs = sr.s;
+                w.scs = sc.s;
+                w.R = g.R[k];
+                w.C = g.C[k];
+                w.offR = g.offR[k];
+                w.offC = g.offC[k];
+                w.rns = 1.0f / (float)w.ns;
+                w.rsc = 1.0f / (float)sc.len;
+                base += (3 + (k == L)) * w.ns;
+            }
+            s_wl[k] = w;
+        }
+    }
     /* ---------------- F: every analysis level of the tile in LDS ---------------- */
     const int H0 = g.R[0], W0 = g.C[0];
     float* P = g.P + (int64_t)b * g.PR * g.PC;
@@ -545,19 +572,15 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     for (int k = 1; k <= L; ++k) nwin += (3 + (k == L)) * axr.sv[k].len * axc.sv[k].len;
     auto win_src = [&](int e) -> const float* { /* the packed coefficient behind window word e */
         int k = 1;
-        for (; k < L; ++k) {
-            const int c = 3 * axr.sv[k].len * axc.sv[k].len;
-            if (e < c) break;
-            e -= c;
-        }
-        const SmIvl sr = axr.sv[k], sc = axc.sv[k];
-        const int ns = sr.len * sc.len;
+        while (k < L && e >= s_wl[k + 1].base) ++k;
+        const WinLvl& w = s_wl[k];
+        e -= w.base;
         int pl, idx, mr, mc;
-        sm_divmod(e, ns, 1.0f / (float)ns, &pl, &idx);
-        sm_divmod(idx, sc.len, 1.0f / (float)sc.len, &mr, &mc);
-        const int r = sm_wrap(sr.s + mr, g.R[k]), c = sm_wrap(sc.s + mc, g.C[k]);
-        const int rr = pl == 1 || pl == 2 ? g.offR[k] + r : r;
-        const int cc = pl == 0 || pl == 2 ? g.offC[k] + c : c;
+        sm_divmod(e, w.ns, w.rns, &pl, &idx);
+        sm_divmod(idx, w.scl, w.rsc, &mr, &mc);
+        const int r = sm_wrap(w.srs + mr, w.R), c = sm_wrap(w.scs + mc, w.C);
+        const int rr = pl == 1 || pl == 2 ? w.offR + r : r;
+        const int cc = pl == 0 || pl == 2 ? w.offC + c : c;
         return P + (int64_t)rr * g.PC + cc;
     };
 
