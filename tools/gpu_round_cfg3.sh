@@ -1,6 +1,9 @@
+#!/bin/bash
+# cfg3 refresh after a k_small change: smoke, the whole GPU suite, cfg3 PMC (copied into the box's profiles/), the cfg3 bench line and kernel trace.
+# Usage: gpurun --timeout 1200 -- bash tools/gpu_round_cfg3.sh TAG
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$ROOT"; OUT=$ROOT/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
-TAG=r05c
+TAG=${1:-r05c}
 echo "== smoke"; timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1 || { tail -20 "$OUT/smoke_$TAG.log"; exit 1; }
 tail -1 "$OUT/smoke_$TAG.log"
 echo "== pytest -m gpu"; timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1 || { tail -40 "$OUT/pytest_gpu_$TAG.log"; exit 1; }
