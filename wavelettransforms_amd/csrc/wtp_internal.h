@@ -28,7 +28,8 @@ constexpr int M_SAMPLE = 4096;      /* k_resident: every workgroup draws it befo
 constexpr int M_SAMPLE_WIN = 65536;
 constexpr int SAMPLE_GROUP = 16;   /* contiguous keys per sample group */
 constexpr int NSUB_MAX = 1024;     /* buckets over (kl, kh]: 64..1024 per segment (SegDesc) */
-constexpr int RES_NSUB_LOG2 = 10;  /* k_resident: 1024 buckets over (kl, kh] (4096 measured slower: 8 KB more reads per workgroup) */
+constexpr int RES_NSUB_LOG2 = 10;  /* k_resident: 1024 buckets over (kl, kh] (4096 measured slower: 8 KB more reads per
+                                     * workgroup; 2048 with the selectors, round 5: 26.2 against 25.8 us) */
 constexpr int RES_NSUB = 1 << RES_NSUB_LOG2;
 constexpr int BUCKET_MAX = 8192;   /* keys per bucket (two buckets are staged in LDS)       */
 constexpr int BUCKET_MAX_DWT = 1 << 16; /* DWT segments: 64 wide buckets, one select per segment */
