@@ -527,27 +527,39 @@ def main():
                       % (prof_calls, dom_kernel, nsteps))
 
     # ------------------------------------------------ cold Infinity Cache (MALL)
+    # two cold states: "write" -- a 512 MiB write to another buffer between steps, which leaves the
+    # 256 MiB Infinity Cache full of that buffer's DIRTY lines (every line the step brings in first
+    # writes one of them back to HBM); "read" -- a 512 MiB read of another buffer, which leaves it
+    # full of clean lines (the step's data comes from HBM, nothing else is written back)
     cold = None
     if not args.no_cold and not sharded and xs:
         flush = torch.empty(512 << 20 >> 2, dtype=torch.float32, device=dev)
-        cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.cold_reps)]
-        for a, b in cev:
-            flush.fill_(1.0)
-            a.record()
-            step()
-            b.record()
-        torch.cuda.synchronize()
-        cms = np.array([a.elapsed_time(b) for a, b in cev])
-        cold = {"ms_per_step_p50": float(np.median(cms)), "ms_per_step_p10": float(np.percentile(cms, 10)),
-                "ms_per_step_p90": float(np.percentile(cms, 90)), "reps": len(cev),
-                "note": "a 512 MiB write between steps evicts the 256 MiB Infinity Cache; eager launches, "
-                        "per-step HIP events (include the launch's dispatch gap)"}
-        if resident or small:
-            cspans = stamp_spans(args.cold_reps, before=lambda: flush.fill_(1.0))
-            cus = float(np.mean(cspans))
-            cold[dom + "_us"] = cus
-            cold["roofline_frac"] = dom_bytes / (cus * 1e-6) / 1e9 / HBM_PEAK_GBS
+        flush.fill_(1.0)
+        cold = {}
+        for kind, fl in (("write", lambda: flush.fill_(1.0)), ("read", lambda: flush.sum())):
+            cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(args.cold_reps)]
+            for a, b in cev:
+                fl()
+                a.record()
+                step()
+                b.record()
+            torch.cuda.synchronize()
+            cms = np.array([a.elapsed_time(b) for a, b in cev])
+            c = {"ms_per_step_p50": float(np.median(cms)), "ms_per_step_p10": float(np.percentile(cms, 10)),
+                 "ms_per_step_p90": float(np.percentile(cms, 90)), "reps": len(cev),
+                 "note": ("a 512 MiB %s of another buffer between steps evicts the 256 MiB Infinity Cache "
+                          "(%s); eager launches, per-step HIP events (include the launch's dispatch gap)"
+                          % (kind, "leaving it full of dirty lines" if kind == "write" else "clean lines"))}
+            if resident or small:
+                cspans = stamp_spans(args.cold_reps, before=fl)
+                cus = float(np.mean(cspans))
+                c[dom + "_us"] = cus
+                c["roofline_frac"] = dom_bytes / (cus * 1e-6) / 1e9 / HBM_PEAK_GBS
+            if kind == "write":
+                cold.update(c)
+            else:
+                cold["after_read_flush"] = c
         del flush
 
     # ------------------------------------------------- N > 1 legs (cfg4 split, replicas)

@@ -41,6 +41,21 @@ def test_lpt_plan_resnet18():
             assert max(plan.bytes_received(r) for r in range(world)) <= 4 * 11_166_912 + 20 * REC_BYTES + 8 * 12
 
 
+def test_lpt_plan_allgather_layout():
+    """exchange="allgather": the same LPT table, every region padded to one 16-byte-aligned stride
+    and placed at r * stride (the in-place all_gather_into_tensor layout)"""
+    shapes = [s for _, s, *_ in W.resnet18_tensors(0)]
+    for world in (1, 2, 3, 4, 8):
+        p2p, ag = ShardPlan(shapes, world), ShardPlan(shapes, world, "allgather")
+        assert ag.mine == p2p.mine and ag.offset == p2p.offset and ag.size == p2p.size
+        assert ag.stride % 4 == 0 and ag.stride >= max(ag.size)
+        assert ag.base == [r * ag.stride for r in range(world)] and ag.total == world * ag.stride
+        for r in range(world):
+            assert ag.bytes_received(r) == 4 * ag.stride * (world - 1) >= p2p.bytes_received(r)
+    with pytest.raises(ValueError):
+        ShardPlan(shapes, 2, "ring")
+
+
 def _oracle_prune(wavelet, level, pct):
     from oracle import oracle as O
 
@@ -62,7 +77,7 @@ def _tensors(ntens):
     return ts if ntens is None else ts[:ntens]
 
 
-def _worker(rank, world, port, q, ntens=None):
+def _worker(rank, world, port, q, ntens=None, kind="p2p"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -70,7 +85,7 @@ def _worker(rank, world, port, q, ntens=None):
         ts = _tensors(ntens)
         xs = [torch.from_numpy(W.synth_numpy(s, seed, tid, e)) for _, s, seed, tid, e in ts]
         full, recs, plan = prune_sharded(xs, "haar", 2, 61.8, _oracle_prune("haar", 2, 61.8),
-                                         device=torch.device("cpu"))
+                                         device=torch.device("cpu"), exchange_kind=kind)
         q.put((rank, [f.numpy().copy() for f in full], recs, plan.mine))
     finally:
         dist.destroy_process_group()
@@ -82,11 +97,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_world(world, ntens=None):
+def _run_world(world, ntens=None, kind="p2p"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, ntens)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, ntens, kind)) for r in range(world)]
     for p in procs:
         p.start()
     import queue
@@ -103,10 +118,11 @@ def _run_world(world, ntens=None):
 
 
 @pytest.mark.timeout(300)
-def test_prune_sharded_gloo_world2():
+@pytest.mark.parametrize("kind", ["p2p", "allgather"])
+def test_prune_sharded_gloo_world2(kind):
     from oracle import oracle as O
     world = 2
-    got = _run_world(world)
+    got = _run_world(world, kind=kind)
     ts = _tensors(None)
     refs = [O.prune_tensor(W.synth_numpy(s, seed, tid, e), "haar", 2, 61.8) for _, s, seed, tid, e in ts]
     mines = [g[3] for g in got]
@@ -119,11 +135,13 @@ def test_prune_sharded_gloo_world2():
 
 
 @pytest.mark.timeout(300)
-def test_prune_sharded_gloo_more_ranks_than_tensors():
+@pytest.mark.parametrize("kind", ["p2p", "allgather"])
+def test_prune_sharded_gloo_more_ranks_than_tensors(kind):
     """world 3 over 2 tensors: one rank owns nothing, its region is empty and no zero-element
-    point-to-point operation is posted for it; every rank still ends with the whole result"""
+    point-to-point operation is posted for it (p2p; the padded all-gather carries its stride of
+    padding); every rank still ends with the whole result"""
     from oracle import oracle as O
-    got = _run_world(3, ntens=2)
+    got = _run_world(3, ntens=2, kind=kind)
     ts = _tensors(2)
     refs = [O.prune_tensor(W.synth_numpy(s, seed, tid, e), "haar", 2, 61.8) for _, s, seed, tid, e in ts]
     mines = got[0][3]

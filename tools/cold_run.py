@@ -17,6 +17,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3"])
     ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--flush", default="write", choices=["write", "read", "clean"],
+                    help="write: a 512 MiB write before each prune (the Infinity Cache then holds dirty "
+                         "lines of another buffer); read: a 512 MiB read (clean lines of another buffer); "
+                         "clean: the write, then the read of a third buffer")
     a = ap.parse_args()
     import torch
     from wavelettransforms_amd import engine
@@ -29,14 +33,18 @@ def main():
     xs = [engine.synth(s, seed, tid, e, device=dev) for (_, s, seed, tid, e) in ts]
     outs = [torch.empty_like(x) for x in xs]
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    flush_r = torch.ones(128 << 20, dtype=torch.float32, device=dev)
     for _ in range(3):
         engine.launch(xs, wavelet, level, pct, outs=outs, carry_level=False)
     torch.cuda.synchronize()
     for _ in range(a.steps):
-        flush.fill_(1)
+        if a.flush in ("write", "clean"):
+            flush.fill_(1)
+        if a.flush in ("read", "clean"):
+            flush_r.sum()
         engine.launch(xs, wavelet, level, pct, outs=outs, carry_level=False)
     torch.cuda.synchronize()
-    print("cold leg done: %d steps of %s" % (a.steps, a.config))
+    print("cold leg done: %d steps of %s, flush %s" % (a.steps, a.config, a.flush))
 
 
 if __name__ == "__main__":

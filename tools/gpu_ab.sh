@@ -21,16 +21,19 @@ for c in $CFGS; do
   X=""; [ $c = cfg5 ] && X="--steps 10 --warmup 2 --replays 10"
   for v in new base new base; do
     L=${NEW_LIB:-}; [ $v = base ] && L=${BASE_LIB:-$(pwd)/tools/ab/libwtprune_base.so}
-    WTP_LIB_PATH=$L timeout -k 10 300 python bench.py --config $c --no-cpu --no-cold $X > $OUT/b_${TAG}_${c}_$v.log 2>&1 || { tail -20 $OUT/b_${TAG}_${c}_$v.log; exit 1; }
+    NC="--no-cold"; [ -n "$COLD" ] && NC=""
+    WTP_LIB_PATH=$L timeout -k 10 300 python bench.py --config $c --no-cpu $NC $X > $OUT/b_${TAG}_${c}_$v.log 2>&1 || { tail -20 $OUT/b_${TAG}_${c}_$v.log; exit 1; }
     python3 -c "
 import json
 d=json.loads([l for l in open('$OUT/b_${TAG}_${c}_$v.log') if l.startswith('{')][-1]); r=d['roofline']
-print('$c', '$v', round(d['ms_per_step']*1e3,2), 'us/step', r.get('kernel'), round(r.get('avg_launch_us') or -1,2), 'frac', round(r.get('frac') or -1,3))"
+cm=d.get('cold_mall') or {}; cr=cm.get('after_read_flush') or {}
+print('$c', '$v', round(d['ms_per_step']*1e3,2), 'us/step', r.get('kernel'), round(r.get('avg_launch_us') or -1,2), 'frac', round(r.get('frac') or -1,3),
+      'cold(write) %.2f us/step span %.2f | cold(read) %.2f span %.2f' % (1e3*cm.get('ms_per_step_p50',0), cm.get(r.get('kernel','')+'_us',0), 1e3*cr.get('ms_per_step_p50',0), cr.get(r.get('kernel','')+'_us',0)) if cm else '')"
   done
 done
 if [ -n "$RESLAB" ]; then
   echo "== reslab"
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/mb/reslab.hip -o /tmp/reslab || exit 1
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I wavelettransforms_amd/csrc tools/mb/reslab.hip -o /tmp/reslab || exit 1
   timeout -k 10 120 /tmp/reslab 50 $OUT/reslab_$TAG.csv > $OUT/reslab_$TAG.log 2>&1 || { echo reslab failed; tail -20 $OUT/reslab_$TAG.log; exit 1; }
   grep -v "184466" $OUT/reslab_$TAG.log | head -30
 fi

@@ -12,7 +12,7 @@ echo "== resident tests"
 timeout -k 10 300 python -u -m pytest tests/test_gpu_resident.py -x -v --timeout 120 --timeout-method thread > "$OUT/res_$TAG.log" 2>&1 || { echo resident tests failed; grep -E "PASS|FAIL|Error|assert" "$OUT/res_$TAG.log" | tail -40; exit 1; }
 tail -1 "$OUT/res_$TAG.log"
 echo "== reslab"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/mb/reslab.hip -o /tmp/reslab && timeout -k 10 120 /tmp/reslab 50 "$OUT/reslab_$TAG.csv" > "$OUT/reslab_$TAG.log" 2>&1 || { echo reslab failed; tail -20 "$OUT/reslab_$TAG.log"; exit 1; }
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I wavelettransforms_amd/csrc tools/mb/reslab.hip -o /tmp/reslab && timeout -k 10 120 /tmp/reslab 50 "$OUT/reslab_$TAG.csv" > "$OUT/reslab_$TAG.log" 2>&1 || { echo reslab failed; tail -20 "$OUT/reslab_$TAG.log"; exit 1; }
 grep -v "184466\|select" "$OUT/reslab_$TAG.log"
 if [ -n "$2" ]; then
 echo "== all gpu tests"

@@ -16,17 +16,29 @@ __device__ unsigned long long g_sprobe[NWG][16];
 #define WTP_WPROBE(i) WTP_RPROBE(12 + (i))
 #define WTP_RTAG(tagv) do { if (threadIdx.x == 0) g_rprobe[blockIdx.x][19] = (unsigned long long)(tagv); } while (0)
 #endif
-#include "../../wavelettransforms_amd/csrc/kernels.hip"
-#include "../../wavelettransforms_amd/csrc/filterbank.hip"
-#include "../../wavelettransforms_amd/csrc/small.hip"
-#include "../../wavelettransforms_amd/csrc/api.hip"
+#include "kernels.hip"  /* -I wavelettransforms_amd/csrc (or a variant copy) */
+#include "filterbank.hip"  /* -I wavelettransforms_amd/csrc (or a variant copy) */
+#include "small.hip"  /* -I wavelettransforms_amd/csrc (or a variant copy) */
+#include "api.hip"  /* -I wavelettransforms_amd/csrc (or a variant copy) */
 #include <cstdio>
 #include <vector>
 #include <algorithm>
+/* cold-cache flushes between reps (argv[3]): 0 none (warm), 1 write 512 MiB (the bench's cold leg:
+ * the Infinity Cache then holds dirty lines of another buffer), 2 read 512 MiB (clean lines of another
+ * buffer), 3 write then read two other 512 MiB buffers (dirty lines written back before the call) */
+__global__ void k_flush_read(const float4* __restrict__ p, size_t n4, float* __restrict__ sink) {
+    float acc = 0.f;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        const float4 v = p[i]; /* plain loads: they allocate in the Infinity Cache */
+        acc += v.x + v.y + v.z + v.w;
+    }
+    if (acc == 1234.5f) sink[0] = acc;
+}
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 50;
+    const int flush = argc > 3 ? atoi(argv[3]) : 0;
     const int64_t shapes[20][4] = {{64,3,7,7},{64,64,3,3},{64,64,3,3},{64,64,3,3},{64,64,3,3},{128,64,1,1},{128,64,3,3},
         {128,128,3,3},{128,128,3,3},{128,128,3,3},{256,128,1,1},{256,128,3,3},{256,256,3,3},{256,256,3,3},{256,256,3,3},
         {512,256,1,1},{512,256,3,3},{512,512,3,3},{512,512,3,3},{512,512,3,3}};
@@ -56,7 +68,12 @@ int main(int argc, char** argv) {
     static unsigned long long pr[NWG][20];
     std::vector<std::vector<double>> ph(18), sel(15), phg[2];
     phg[0].resize(18); phg[1].resize(18);
+    const size_t FL = (size_t)512 << 20;
+    float *fw = nullptr, *fr = nullptr, *sink = nullptr;
+    if (flush) { CK(hipMalloc(&fw, FL)); CK(hipMalloc(&fr, FL)); CK(hipMalloc(&sink, 64)); CK(hipMemset(fr, 0, FL)); }
     for (int r = 0; r < reps; ++r) {
+        if (flush == 1 || flush == 3) CK(hipMemsetAsync(fw, r & 0xff, FL, 0));
+        if (flush == 2 || flush == 3) hipLaunchKernelGGL(k_flush_read, dim3(4096), dim3(256), 0, 0, (const float4*)fr, FL / 16, sink);
         CK(hipEventRecord(a, 0));
         wtp_prune_layers_f32(ts.data(), 20, wid, 5, 50.0, ws, wsb, res, 0);
         CK(hipEventRecord(b, 0));
@@ -120,6 +137,7 @@ int main(int argc, char** argv) {
         if (!f.empty()) printf("in-kernel shader clock (s_memtime / s_memrealtime): median %.2f GHz (min %.2f, max %.2f)\n", f[f.size() / 2], f[0], f.back());
     }
     std::sort(tms.begin(), tms.end());
+    printf("flush mode %d\n", flush);
     printf("k_resident cfg2: median %.2f us (min %.2f) per call, %.1f GB/s algorithmic\n", tms[tms.size() / 2], tms[0],
            8.0 * nw / (tms[tms.size() / 2] * 1e-6) / 1e9);
     const char* names[18] = {"start", "window", "counted", "hist-pub", "B1-arrive", "B1-pass", "selected", "stored",

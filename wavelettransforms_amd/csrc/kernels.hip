@@ -124,12 +124,23 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v
     return t;
 }
 
-/* IT float4 per thread of one chunk (fully populated, 16-byte aligned) */
-template <int IT, int CT = STREAM_THREADS>
+/* IT float4 per thread of one chunk (fully populated, 16-byte aligned).  NT: nontemporal loads
+ * (the `nt` policy bit) -- k_resident's once-read chunk: measured neutral with warm caches and 7 us
+ * shorter behind a 512 MiB write to another buffer (its reads then no longer evict that buffer's
+ * dirty Infinity-Cache lines) */
+template <int IT, int CT = STREAM_THREADS, bool NT = false>
 __device__ __forceinline__ void load_chunk(const float* p, float4 (&v)[IT]) {
     const float4* p4 = reinterpret_cast<const float4*>(p);
+    typedef float f4v __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int it = 0; it < IT; ++it) v[it] = p4[it * CT + threadIdx.x];
+    for (int it = 0; it < IT; ++it) {
+        if (NT) {
+            const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p4 + it * CT + threadIdx.x));
+            v[it] = make_float4(t.x, t.y, t.z, t.w);
+        } else {
+            v[it] = p4[it * CT + threadIdx.x];
+        }
+    }
 }
 
 /* A ragged or unaligned chunk of len elements: element e of slot (it, c) is
@@ -141,7 +152,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ragged_rsrc(const float* p, in
     void* base = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
     return __builtin_amdgcn_make_buffer_rsrc(base, 0, __builtin_amdgcn_readfirstlane(len * 4), 0x00020000);
 }
-template <int IT, int CT = STREAM_THREADS>
+template <int IT, int CT = STREAM_THREADS, bool NT = false>
 __device__ __forceinline__ void load_chunk_ragged(const float* p, int len, float4 (&v)[IT]) {
     const __amdgpu_buffer_rsrc_t r = ragged_rsrc(p, len);
     if ((reinterpret_cast<uintptr_t>(p) & 15) == 0 && (len & 3) == 0) { /* uniform */
@@ -150,7 +161,7 @@ __device__ __forceinline__ void load_chunk_ragged(const float* p, int len, float
         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const u4 q = __builtin_amdgcn_raw_buffer_load_b128(r, 16 * (it * CT + (int)threadIdx.x), 0, 0);
+            const u4 q = __builtin_amdgcn_raw_buffer_load_b128(r, 16 * (it * CT + (int)threadIdx.x), 0, NT ? 2 : 0);
             v[it] = make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w));
         }
         return;
@@ -158,10 +169,10 @@ __device__ __forceinline__ void load_chunk_ragged(const float* p, int len, float
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
         const int e = 4 * (it * CT + (int)threadIdx.x);
-        v[it].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e, 0, 0));
-        v[it].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e + 4, 0, 0));
-        v[it].z = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e + 8, 0, 0));
-        v[it].w = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e + 12, 0, 0));
+        v[it].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e, 0, NT ? 2 : 0));
+        v[it].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e + 4, 0, NT ? 2 : 0));
+        v[it].z = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e + 8, 0, NT ? 2 : 0));
+        v[it].w = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * e + 12, 0, NT ? 2 : 0));
     }
 }
 /* range-checked float4 store: the dwords past the buffer's length are dropped */
@@ -1393,8 +1404,8 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
          * the window is known: the early group's chunks come off HBM first, and their counts,
          * barriers and selects run while the late group's chunks stream */
         if (sd.flags & SEG_LATE) __syncthreads(); /* block-uniform */
-        if (FULL) load_chunk<IT, CT>(sd.data + base, v);
-        else load_chunk_ragged<IT, CT>(sd.data + base, len, v);
+        if (FULL) load_chunk<IT, CT, true>(sd.data + base, v);
+        else load_chunk_ragged<IT, CT, true>(sd.data + base, len, v);
         q = parity_late(qv);
         {   /* clear this workgroup's slice of the idle region (the previous launch's; the next
              * launch works in it): stores behind the chunk's loads */

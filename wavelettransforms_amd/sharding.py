@@ -17,6 +17,13 @@ MI355X each GPU has a direct xGMI link to each of its 7 peers, so the 7 copies o
 ring all-gather pushes every other rank's bytes through one link in turn.  Compute
 and exchange are stream-ordered: nothing waits on the host before it.
 
+A second exchange form is selectable (`exchange="allgather"`, SURVEY.md 8e's north_star wording):
+every region padded to the largest one (rounded to 16 bytes) so that the regions sit at
+r * stride, and ONE all_gather_into_tensor in place (rank r contributes full[r * stride : (r + 1) *
+stride]).  RCCL runs it as a ring over xGMI: each link carries (N - 1) x stride bytes one after
+another, so at N = 8 it moves 7 x 9.4 MB per link where the full mesh moves one region per link
+ -- kept as the fallback and the comparison for the first multi-GPU runs.
+
 The table is computed identically on every rank from the shapes alone.  After the exchange every
 rank holds every record, so a resident launch that timed out on one rank (its tensors' records
 read MODE_FAULT; nothing was stored for them) is seen by all ranks alike: the owners re-run exactly
@@ -52,7 +59,12 @@ class ShardPlan:
     region), then from rec_off[r] its records (16-byte aligned: the kernels update the records'
     8-byte counters in place, and every region starts 16-byte aligned for the float4 paths)."""
 
-    def __init__(self, shapes, world):
+    EXCHANGES = ("p2p", "allgather")
+
+    def __init__(self, shapes, world, exchange="p2p"):
+        if exchange not in self.EXCHANGES:
+            raise ValueError("exchange must be one of %s, got %r" % (self.EXCHANGES, exchange))
+        self.exchange = exchange
         self.shapes = [tuple(s) for s in shapes]
         self.numels = [int(np.prod(s)) if len(s) else 1 for s in self.shapes]
         self.world = world
@@ -67,18 +79,30 @@ class ShardPlan:
         self.max_shard = max(self.loads) if self.loads else 0
         self.rec_off = [_align4(self.loads[r]) for r in range(world)]
         self.size = [self.rec_off[r] + len(self.mine[r]) * REC_WORDS for r in range(world)]
-        self.base = [int(b) for b in np.concatenate([[0], np.cumsum(self.size)[:-1]])] if world else []
-        self.total = int(sum(self.size))
+        if exchange == "allgather":
+            # padded regions at r * stride: the in-place all_gather_into_tensor layout
+            self.stride = _align4(max(self.size)) if world else 0
+            self.base = [r * self.stride for r in range(world)]
+            self.total = self.stride * world
+        else:
+            self.stride = None
+            self.base = [int(b) for b in np.concatenate([[0], np.cumsum(self.size)[:-1]])] if world else []
+            self.total = int(sum(self.size))
 
     def region(self, r):
         return self.base[r], self.base[r] + self.size[r]
 
     def bytes_sent(self, r):
-        """Bytes rank r puts on the wire in one exchange (its region to each peer)."""
+        """Bytes rank r puts on the wire in one exchange: its region to each peer (p2p), or in a
+        ring all-gather (N - 1) padded regions -- its own and the ones it forwards."""
+        if self.exchange == "allgather":
+            return 4 * self.stride * (self.world - 1)
         return 4 * self.size[r] * (self.world - 1)
 
     def bytes_received(self, r):
-        """Bytes rank r receives in one exchange (every other region once)."""
+        """Bytes rank r receives in one exchange (every other region once; padded for allgather)."""
+        if self.exchange == "allgather":
+            return 4 * self.stride * (self.world - 1)
         return 4 * (self.total - self.size[r])
 
 
@@ -130,10 +154,15 @@ class _Shard:
 
 
 def exchange(full, plan, rank, group=None):
-    """The full-mesh all-gather of the regions: this rank's region of `full` goes to every peer and
-    every peer's region lands in place, as ONE group of point-to-point operations (stream-ordered
-    behind the compute that wrote the region; waits for completion)."""
+    """The all-gather of the regions (stream-ordered behind the compute that wrote the region; waits
+    for completion).  plan.exchange "p2p": this rank's region of `full` goes to every peer and every
+    peer's region lands in place, as ONE group of point-to-point operations; "allgather": ONE
+    in-place all_gather_into_tensor of the padded regions."""
     if plan.world == 1:
+        return
+    if plan.exchange == "allgather":
+        b0 = plan.base[rank]
+        dist.all_gather_into_tensor(full[:plan.total], full[b0:b0 + plan.stride], group=group)
         return
     b0, b1 = plan.region(rank)
     mine = full[b0:b1]
@@ -177,14 +206,15 @@ def assemble(full, plan):
     return out, recs
 
 
-def prune_sharded(weights, wavelet, level, pct, prune_fn=None, group=None, device=None):
+def prune_sharded(weights, wavelet, level, pct, prune_fn=None, group=None, device=None, exchange_kind="p2p"):
     """weights: list of tensors (the same list on every rank).  prune_fn=None runs this rank's share
     on the GPU (engine.launch, one batched launch sequence, carry_level=False as wavelet_pruning
     does); a test double prune_fn(inputs, out_views) -> list of record dicts may replace it.
+    exchange_kind: "p2p" (full mesh, unpadded) or "allgather" (padded, one all_gather_into_tensor).
     Returns (all pruned tensors on every rank, per-layer records, plan)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    plan = ShardPlan([w.shape for w in weights], world)
+    plan = ShardPlan([w.shape for w in weights], world, exchange_kind)
     sh = _Shard(weights, plan, rank, device or weights[0].device)
     if sh.mine:
         sh.run(sh.mine, wavelet, level, pct, prune_fn)
