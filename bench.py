@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--frame-apart", action="store_true",
                     help="the frame of edge tiles in a launch of its own (wtp_set_interior(2); A/B only)")
     ap.add_argument("--no-rocprof", action="store_true", help="skip the in-run rocprofv3 kernel-stats child")
+    ap.add_argument("--exchange", default="p2p", choices=["p2p", "allgather"],
+                    help="N > 1 cfg4 reassembly: full-mesh point-to-point copies of the unpadded regions (default) "
+                         "or one in-place all_gather_into_tensor of the padded regions")
     ap.add_argument("--profile-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -290,7 +293,7 @@ def main():
     if args.config == "cfg5":
         mine = model[rank * per:(rank + 1) * per]               # cfg5: the blocks split over the ranks
     elif sharded:
-        plan = ShardPlan([s for (s, *_) in model], world)
+        plan = ShardPlan([s for (s, *_) in model], world, args.exchange)
         mine = [model[i] for i in plan.mine[rank]]
     else:
         mine = model
@@ -576,24 +579,31 @@ def main():
         for _ in range(3):
             replica()
         t_rep = timed(Kc, replica) / Kc * 1e3
-        multi = {"cfg4_one_model": {"end_to_end_ms": ms_per_step, "compute_ms_max_rank": t_comp,
+        xname = "batch_isend_irecv" if args.exchange == "p2p" else "all_gather_into_tensor"
+        multi = {"cfg4_one_model": {"exchange": args.exchange, "end_to_end_ms": ms_per_step, "compute_ms_max_rank": t_comp,
                                     "all_gather_ms": t_gath, "max_rank_weights": int(plan.max_shard),
                                     "bytes_sent_this_rank": plan.bytes_sent(rank),
                                     "bytes_received_this_rank": plan.bytes_received(rank),
                                     "bytes_received_max_rank": max(plan.bytes_received(r) for r in range(world)),
                                     "largest_region_bytes": 4 * max(plan.size),
-                                    "per_link_estimate_us": 4 * max(plan.size) / XGMI_LINK_GBS / 1e3,
-                                    "exchange_status": (("rehearsal: batch_isend_irecv over %s with every rank on one "
+                                    "per_link_estimate_us": (4 * max(plan.size) / XGMI_LINK_GBS / 1e3 if args.exchange == "p2p"
+                                                             else 4 * plan.stride * (world - 1) / XGMI_LINK_GBS / 1e3),
+                                    "exchange_status": (("rehearsal: %s over %s with every rank on one "
                                                          "GPU, a functional check; RCCL at N > 1 is not measured by "
-                                                         "this line" % dist.get_backend()) if rehearsal else
-                                                        ("batch_isend_irecv over %s (RCCL on ROCm) across %d GPUs, "
-                                                         "measured by this line" % (dist.get_backend(), world))),
-                                    "per_link_estimate_note": "assumes every peer pair on its own xGMI link at %.0f "
-                                                              "GB/s, the largest region the longest copy" % XGMI_LINK_GBS,
-                                    "note": "LPT layer shards pruned in place into the flat state_dict buffer, then "
-                                            "ONE full-mesh exchange of the unpadded regions (weights + records; "
-                                            "batch_isend_irecv = one RCCL group of point-to-point copies, one per "
-                                            "xGMI peer link); eager launches"},
+                                                         "this line" % (xname, dist.get_backend())) if rehearsal else
+                                                        ("%s over %s (RCCL on ROCm) across %d GPUs, "
+                                                         "measured by this line" % (xname, dist.get_backend(), world))),
+                                    "per_link_estimate_note": ("assumes every peer pair on its own xGMI link at %.0f "
+                                                               "GB/s, the largest region the longest copy" % XGMI_LINK_GBS
+                                                               if args.exchange == "p2p" else
+                                                               "ring all-gather: (N - 1) padded regions through one "
+                                                               "xGMI link at %.0f GB/s" % XGMI_LINK_GBS),
+                                    "note": ("LPT layer shards pruned in place into the flat state_dict buffer, then "
+                                             + ("ONE full-mesh exchange of the unpadded regions (weights + records; "
+                                                "batch_isend_irecv = one RCCL group of point-to-point copies, one per "
+                                                "xGMI peer link)" if args.exchange == "p2p" else
+                                                "ONE in-place all_gather_into_tensor of the regions padded to the "
+                                                "largest (weights + records)") + "; eager launches")},
                  "replicas": {"value": world * n_model / (t_rep * 1e-3), "ms_per_step": t_rep, "scaling": "weak",
                               "note": "every rank prunes its own full model, no collective"}}
 
@@ -643,7 +653,8 @@ def main():
                        "weights_this_rank": n_w, "coeffs_this_rank": pop, "tensors": len(model),
                        "eff_levels": sorted({r["eff_level"] for r in recs}),
                        "graph_steps": G if graph is not None else 0,
-                       "parallelism": ("lpt-layer-shard%d+allgather" % world if sharded
+                       "parallelism": ("lpt-layer-shard%d+%s" % (world, "allgather-p2p" if args.exchange == "p2p"
+                                                                 else "allgather-ring") if sharded
                                        else ("block-split%d" % world if world > 1 else "single")),
                        "transform": "1-D flattened (extension)" if args.flatten else "2-D over (kh, kw) (reference)"},
             "value_source": value_src,

@@ -176,7 +176,7 @@ int wtp_resident_capacity(void); /* 0 if the current device cannot host the resi
  * launch whose workgroups were not all resident at once times out there and stores NOTHING for
  * the tensors concerned (inputs and outputs untouched): their records read path == 99
  * (WTP_PATH_FAULT), and the caller re-runs exactly those tensors with wtp_set_resident(0).
- * Default 200000, at most 40000000 (larger values are clamped: the bound is kept in 32-bit
+ * Default 2000 (about 75x a full ResNet-18 resident launch), at most 40000000 (larger values are clamped: the bound is kept in 32-bit
  * ticks of the 100 MHz wall clock); tests lower it to force the fault path. */
 unsigned wtp_set_resident_timeout_us(unsigned us);
 #define WTP_PATH_FAULT 99
@@ -184,11 +184,8 @@ unsigned wtp_set_resident_timeout_us(unsigned us);
  * group's percentile selection on a side stream of the library's (one per device and caller
  * stream, non-blocking, created on first use), overlapping the next group's forward transform;
  * the caller's stream waits for it before that group's inverse, so the call stays ordered on
- * the caller's stream (graph capture included).  Mode 2: every group's forward and inverse on a
- * lane stream of its own (group g + 1's forward starts once group g's first two levels are done),
- * the selections on the side stream, every lane and the side stream joined back into the
- * caller's stream at the end of the call.  Mode 0: everything on the caller's stream.  Returns
- * the previous mode (process-wide). */
+ * the caller's stream (graph capture included).  Mode 0: everything on the caller's stream; any
+ * other value is rejected (WTP_EARG).  Returns the previous mode (process-wide). */
 int wtp_set_pipeline(int mode);
 /* The filter-bank levels run their interior tiles (input window inside the image, full tile)
  * in kernels compiled without the edge forms and the frame of edge tiles in the same kernels'

@@ -71,6 +71,26 @@ def test_cfg2_in_place(eng, mode):
         _same(o.cpu().numpy(), ref, r, rr)
 
 
+def test_cfg2_in_place_full_scan_with_selectors(eng):
+    """in place, pct 100 sends every shared segment down the full-scan path while its
+    selector workgroup is in the grid.  The selector publishes the threshold before it counts the
+    zeros over the segment's input, which the data workgroups are then overwriting; the count holds
+    because where(|x| < thr, 0, x) maps every key below bits(thr) to +0 (still below) and leaves the
+    rest -- this test pins that invariant against the oracle."""
+    ts = G.W.resnet18_tensors(0)
+    for pct in (100.0, 99.99999):
+        xs = [eng.synth(s, seed, tid, e) for _, s, seed, tid, e in ts]
+        refs = [O.prune_tensor(x.cpu().numpy(), "bior3.3", 5, pct) for x in xs]
+        outs, res = eng.prune(xs, "bior3.3", 5, pct, outs=xs, carry_level=False)
+        full = 0
+        for (_, s, *_), x, o, r, (ref, rr) in zip(ts, xs, outs, res, refs):
+            assert o.data_ptr() == x.data_ptr()
+            _same(o.cpu().numpy(), ref, r, rr)
+            full += r["path"] == 3 and int(np.prod(s)) > RES_CHUNK
+        if pct == 100.0:
+            assert full > 0
+
+
 def _miss_input(n, seed):
     """Values whose sampled positions (SAMPLE_GROUP-float groups spread evenly) hold 1.0 while
     the rest are ~2.0: the sample window misses the true order statistics."""
@@ -156,7 +176,8 @@ def test_shared_segments_without_room_for_selectors(eng, in_place):
     cap = eng.resident_capacity()
     n = 10 * RES_CHUNK - 3
     xs = [eng.synth((n,), 41, j, 27 + (j % 3)) for j in range(24)]
-    assert 24 * 10 <= cap < 24 * 10 + 24
+    if not (24 * 10 <= cap < 24 * 10 + 24):  # the case needs a 240..263-CU part (MI355X: 256)
+        pytest.skip("resident capacity %d: no 240-chunk grid without room for 24 selectors" % cap)
     hosts = [x.cpu().numpy() for x in xs]
     outs, res = eng.prune(xs, "bior3.3", 5, 61.8, outs=xs if in_place else None, carry_level=False)
     for h, o, r in zip(hosts, outs, res):
@@ -252,6 +273,98 @@ def test_workspace_per_stream(eng):
         for h, o, r in zip(host, outs, eng.decode(res, len(outs))):
             ref, rr = O.prune_tensor(sign * h, "bior3.3", 5, 37.5)
             _same(o.cpu().numpy(), ref, r, rr)
+
+
+def _finish_with_retry(eng, xs, outs, res, wavelet, level, pct):
+    """engine.prune's fault handling for a launch made elsewhere: the tensors whose resident launch
+    timed out (nothing stored) are re-run once in the three-launch form; returns (records, faults)."""
+    n = len(xs)
+    bad = eng.fault_mask(res, n)
+    recs = None
+    if bad.any():
+        idx = [i for i in range(n) if bad[i]]
+        merged = res.clone().view(n, -1)
+        _, r2 = eng.launch([xs[i] for i in idx], wavelet, level, pct, outs=[outs[i] for i in idx],
+                           carry_level=False, no_resident=True)
+        merged[idx] = r2.view(len(idx), -1)
+        res = merged.view(-1)
+    recs = eng.decode(res, n)
+    return recs, int(bad.sum())
+
+
+def test_two_full_calls_on_two_streams(eng):
+    """two full cfg2 calls at once on two streams -- each a 240-workgroup
+    k_resident launch of one workgroup per CU, together more than the chip's 256 CUs hold.  Whatever
+    the hardware interleaves, both calls end bit-exact against the oracle, a tensor whose launch was
+    not co-resident faults within the wait bound (2 ms) and is re-run, and the pair completes in
+    well under the round-5 bound of 200 ms."""
+    import time
+    ts = G.W.resnet18_tensors(0)
+    host = [G.W.synth_numpy(s, seed, tid, e) for _, s, seed, tid, e in ts]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    xa = [_dev(x) for x in host]
+    xb = [_dev(-x) for x in host]
+    for s, xs in ((s1, xa), (s2, xb)):  # workspaces exist before the timed pair
+        with torch.cuda.stream(s):
+            eng.launch(xs, "bior3.3", 5, 50.0, carry_level=False, stream=s)
+    torch.cuda.synchronize()
+    worst, faults = 0.0, 0
+    for rep in range(5):
+        t0 = time.perf_counter()
+        got = {}
+        for name, s, xs in (("a", s1, xa), ("b", s2, xb)):
+            with torch.cuda.stream(s):
+                got[name] = eng.launch(xs, "bior3.3", 5, 50.0, carry_level=False, stream=s)
+        torch.cuda.synchronize()
+        recs = {}
+        for name, xs in (("a", xa), ("b", xb)):
+            outs, res = got[name]
+            recs[name], f = _finish_with_retry(eng, xs, outs, res, "bior3.3", 5, 50.0)
+            faults += f
+        torch.cuda.synchronize()
+        worst = max(worst, time.perf_counter() - t0)
+        if rep == 0 or rep == 4:
+            for name, sign in (("a", 1.0), ("b", -1.0)):
+                outs = got[name][0]
+                for h, o, r in zip(host, outs, recs[name]):
+                    ref, rr = O.prune_tensor(sign * h, "bior3.3", 5, 50.0)
+                    _same(o.cpu().numpy(), ref, r, rr)
+    print("two concurrent cfg2 calls: worst pair %.2f ms, %d faulted tensors over 5 pairs" % (worst * 1e3, faults))
+    assert worst < 0.05, worst
+
+
+def test_resident_beside_long_kernels(eng):
+    """a cfg2 call on one stream while another stream runs ~5 ms of grid-filling
+    elementwise kernels (2 GiB in place, 8 passes): bit-exact against the oracle, and the call ends
+    within the wait bound plus a re-run of the call (events on its own stream)."""
+    ts = G.W.resnet18_tensors(0)
+    host = [G.W.synth_numpy(s, seed, tid, e) for _, s, seed, tid, e in ts]
+    xs = [_dev(x) for x in host]
+    big = torch.ones(512 << 20, dtype=torch.float32, device="cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(s2):
+        eng.launch(xs, "bior3.3", 5, 50.0, carry_level=False, stream=s2)
+    torch.cuda.synchronize()
+    worst, faults = 0.0, 0
+    for rep in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s1):
+            for _ in range(8):
+                big.mul_(1.0)
+        with torch.cuda.stream(s2):
+            torch.cuda._sleep(200_000)  # let the other stream's kernels take the CUs first
+            a.record(s2)
+            outs, res = eng.launch(xs, "bior3.3", 5, 50.0, carry_level=False, stream=s2)
+            b.record(s2)
+        torch.cuda.synchronize()
+        recs, f = _finish_with_retry(eng, xs, outs, res, "bior3.3", 5, 50.0)
+        faults += f
+        worst = max(worst, a.elapsed_time(b))
+        for h, o, r in zip(host, outs, recs):
+            ref, rr = O.prune_tensor(h, "bior3.3", 5, 50.0)
+            _same(o.cpu().numpy(), ref, r, rr)
+    print("cfg2 beside 8 x 2 GiB elementwise passes: worst call %.3f ms, %d faulted tensors" % (worst, faults))
+    assert worst < 50.0, worst
 
 
 def test_outs_validated(eng):

@@ -92,11 +92,11 @@ def test_workspace_size_covers_both_level_modes():
 
 
 def test_mode_switches_validate_and_return_the_previous_mode():
-    """wtp_set_resident (0 or 1) / wtp_set_pipeline (0, 1 or 2): the previous mode returned,
+    """wtp_set_resident (0 or 1) / wtp_set_pipeline (0 or 1): the previous mode returned,
     anything else rejected with WTP_EARG and the mode left as it was (host logic only, no device
     work)."""
     L = N.lib()
-    for setter, top in ((L.wtp_set_resident, 1), (L.wtp_set_pipeline, 2)):
+    for setter, top in ((L.wtp_set_resident, 1), (L.wtp_set_pipeline, 1)):
         prev = setter(0)
         assert prev in range(top + 1)
         assert setter(1) == 0

@@ -27,6 +27,7 @@ for v in ${VARIANTS:-base}; do
     cd /tmp
     timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/p_${v}_${m}_$r" -o run --output-format csv -- /tmp/rvbin_$v 60 /dev/null $m > "$OUT/l_${v}_${m}_$r.log" 2>&1 || { echo "run $v $m failed"; tail -5 "$OUT/l_${v}_${m}_$r.log"; exit 1; }
     cd "$ROOT"
+    grep "k_resident cfg2" "$OUT/l_${v}_${m}_$r.log" | sed "s/^/  $v flush $m rep $r event-timed: /"
     python3 - "$OUT/p_${v}_${m}_$r/run_kernel_stats.csv" "$v" "$m" "$r" <<'PY'
 import csv, sys
 for row in csv.DictReader(open(sys.argv[1])):

@@ -292,8 +292,7 @@ struct Chain {
  * chains is ONE tiled launch (filterbank.hip) where the level is large enough, else the two
  * per-point passes of that chain.  Each approximation ping-pongs between the chain's own temps
  * so no launch reads what it writes. */
-void forward_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s, int mark_level = 0,
-                    hipEvent_t mark = nullptr) {
+void forward_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s) {
     int maxL = 0;
     for (const Chain& c : cs) maxL = std::max(maxL, c.p->L);
     std::vector<const float*> cur(cs.size());
@@ -322,9 +321,7 @@ void forward_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s,
             }
         }
         if (!items.empty()) launch_fwd_levels(items.data(), (int)items.size(), tp, s);
-        if (mark && (k == mark_level || (k == maxL && maxL < mark_level))) (void)hipEventRecord(mark, s);
     }
-    if (mark && maxL == 0) (void)hipEventRecord(mark, s);
 }
 
 /* pywt.waverec2 (dwt_pruning.py:75-77) of every chain from its packed layout, thresholding the
@@ -566,7 +563,7 @@ int wtp_resident_capacity(void) { return resident_capacity(); }
 int wtp_set_interior(int mode) { return fb_set_interior(mode); }
 
 int wtp_set_pipeline(int mode) {
-    if (mode < 0 || mode > 2) return fail(WTP_EARG, -1, "bad pipeline mode %d", mode);
+    if (mode < 0 || mode > 1) return fail(WTP_EARG, -1, "bad pipeline mode %d", mode);
     return g_pipeline.exchange(mode);
 }
 unsigned wtp_set_resident_timeout_us(unsigned us) { return set_resident_timeout_us(us); }
@@ -601,11 +598,10 @@ int wtp_workspace_init(void* ws, size_t bytes, wtp_stream_t stream) {
 struct SidePipe {
     hipStream_t side = nullptr;
     std::vector<hipEvent_t> ev;
-    std::vector<hipStream_t> lanes; /* wtp_set_pipeline(2): one per launch group of DWT segments */
 };
 std::mutex g_pipe_mu;
 std::map<std::pair<int, hipStream_t>, SidePipe> g_pipes;
-SidePipe* side_pipe(hipStream_t s, int nev, int nlanes = 0) {
+SidePipe* side_pipe(hipStream_t s, int nev) {
     /* the side stream must live on the caller's stream's device: when that is not the current
      * device (the caller set no device guard) the call keeps the single-stream form */
     int dev = 0, sdev = 0;
@@ -621,11 +617,6 @@ SidePipe* side_pipe(hipStream_t s, int nev, int nlanes = 0) {
         hipEvent_t e;
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
         sp.ev.push_back(e);
-    }
-    while ((int)sp.lanes.size() < nlanes) {
-        hipStream_t l;
-        if (hipStreamCreateWithFlags(&l, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        sp.lanes.push_back(l);
     }
     return &sp;
 }
@@ -690,15 +681,14 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     int dwt_groups = 0;
     for (const auto& gc : gchains) dwt_groups += !gc.empty();
     const int pmode = dwt_groups > 1 ? g_pipeline.load(std::memory_order_relaxed) : 0;
-    /* mode 2 (lanes): events [0] the fork, per group g at 1 + 7 g: the forward's stagger mark,
-     * forward done, selection done, lane done, and the caller's-stream relays of the first three
-     * (EV_*); the side stream's end last */
-    enum { EV_MARK = 1, EV_FDONE, EV_SDONE, EV_LDONE, EV_MARK_R, EV_FDONE_R, EV_SDONE_R, EV_PER = 7 };
-    const int nev = pmode == 2 ? 2 + EV_PER * ngroups : 2 * ngroups + 1;
-    SidePipe* pipe = pmode ? side_pipe(s, nev, pmode == 2 ? ngroups : 0) : nullptr;
-    const bool lanes = pipe && pmode == 2;
+    /* events 2g (group g's forward done) and 2g + 1 (its selection done); the last one joins the
+     * side stream back on an error path.  (Round 5's mode 2 -- each group's levels on a lane
+     * stream of its own -- measured slower and was removed in round 6; its capture-crash
+     * bisection is kept in tools/lanes_capture_diag.py and DESIGN.md.) */
+    const int nev = 2 * ngroups + 1;
+    SidePipe* pipe = pmode ? side_pipe(s, nev) : nullptr;
     const hipStream_t ss = pipe ? pipe->side : s; /* the selection's stream */
-    /* an error after the first fork still joins every forked stream back into the caller's (an
+    /* an error after the first fork still joins the side stream back into the caller's (an
      * unjoined fork invalidates a capture, and eagerly the caller may free what it still reads) */
     bool forked = false;
     auto fail_joined = [&](int t, const char* msg) {
@@ -706,43 +696,9 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             hipEvent_t e = pipe->ev[nev - 1];
             (void)hipEventRecord(e, ss);
             (void)hipStreamWaitEvent(s, e, 0);
-            if (lanes)
-                for (int gi = 0; gi < ngroups; ++gi) {
-                    (void)hipEventRecord(pipe->ev[EV_LDONE + EV_PER * gi], pipe->lanes[gi]);
-                    (void)hipStreamWaitEvent(s, pipe->ev[EV_LDONE + EV_PER * gi], 0);
-                }
         }
         return fail(WTP_EHIP, t, "%s", msg);
     };
-    /* the lanes' stagger: group g + 1's forward starts once group g's first FB_STAGGER levels are
-     * done, so one group's latency-bound small levels and its selection run beside the next group's
-     * large ones */
-    constexpr int FB_STAGGER = 2;
-    /* Every dependency between two forked streams is relayed through the caller's stream: it waits
-     * for the producer's event and records a relay event the consumer waits for.  A captured graph
-     * whose side stream waits on a lane's event while that lane waits on the side stream's (the
-     * direct form) segfaults in hipStreamEndCapture on ROCm 7.2 -- reproduced with plain torch
-     * streams and no kernel of ours (tools/lanes_capture_diag.py, torch_side_lane_cross); forked
-     * streams that wait only on the capturing stream's events are the form mode 1 always used. */
-    auto relay = [&](hipEvent_t producer, hipEvent_t r) {
-        return hipStreamWaitEvent(s, producer, 0) == hipSuccess && hipEventRecord(r, s) == hipSuccess;
-    };
-    if (lanes) {
-        if (hipEventRecord(pipe->ev[0], s) != hipSuccess) return fail(WTP_EHIP, -1, "hipEventRecord failed");
-        forked = true;
-        if (hipStreamWaitEvent(ss, pipe->ev[0], 0) != hipSuccess) return fail_joined(-1, "hipStreamWaitEvent failed");
-        hipEvent_t start = pipe->ev[0];
-        for (int gi = 0; gi < ngroups; ++gi) {
-            const hipStream_t L = pipe->lanes[gi];
-            hipEvent_t* e = pipe->ev.data() + EV_PER * gi;
-            if (hipStreamWaitEvent(L, start, 0) != hipSuccess) return fail_joined(-1, "hipStreamWaitEvent failed");
-            if (gchains[gi].empty()) continue;
-            forward_chains(gchains[gi], tp, L, FB_STAGGER, e[EV_MARK]);
-            if (hipEventRecord(e[EV_FDONE], L) != hipSuccess) return fail_joined(-1, "hipEventRecord failed");
-            if (!relay(e[EV_MARK], e[EV_MARK_R])) return fail_joined(-1, "relay failed");
-            start = e[EV_MARK_R];
-        }
-    }
     if (!pipe) forward_chains(chains, tp, s);
     /* 2. exact percentile selection + level-0 mask, SEG_PER_LAUNCH segments per launch group:
      * one resident launch when every segment of the group is level-0 and the group's chunks fit
@@ -750,12 +706,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     for (int g0 = 0; g0 < ntensors; g0 += SEG_PER_LAUNCH) {
         const int g1 = std::min(ntensors, g0 + SEG_PER_LAUNCH);
         const int gi = g0 / SEG_PER_LAUNCH;
-        if (lanes) { /* this group's selection behind its forward (on its lane), relayed */
-            hipEvent_t* e = pipe->ev.data() + EV_PER * gi;
-            if (!gchains[gi].empty() &&
-                (!relay(e[EV_FDONE], e[EV_FDONE_R]) || hipStreamWaitEvent(ss, e[EV_FDONE_R], 0) != hipSuccess))
-                return fail_joined(-1, "hipStreamWaitEvent failed");
-        } else if (pipe) { /* this group's forward levels on the caller's stream, its selection behind them */
+        if (pipe) { /* this group's forward levels on the caller's stream, its selection behind them */
             forward_chains(gchains[gi], tp, s);
             if (hipEventRecord(pipe->ev[2 * gi], s) != hipSuccess) return fail_joined(-1, "hipEventRecord failed");
             if (hipStreamWaitEvent(ss, pipe->ev[2 * gi], 0) != hipSuccess)
@@ -837,34 +788,13 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             if (inplace) launch_mask_inplace(tab, results, thr_t, ss);
         }
         if (first) stage(4, ss);
-        if (lanes) { /* the group's inverse on its lane behind its selection; the lane joins the caller's stream */
-            if (!gchains[gi].empty()) {
-                const hipStream_t L = pipe->lanes[gi];
-                hipEvent_t* e = pipe->ev.data() + EV_PER * gi;
-                if (hipEventRecord(e[EV_SDONE], ss) != hipSuccess || !relay(e[EV_SDONE], e[EV_SDONE_R]))
-                    return fail_joined(-1, "hipEventRecord failed");
-                if (hipStreamWaitEvent(L, e[EV_SDONE_R], 0) != hipSuccess)
-                    return fail_joined(-1, "hipStreamWaitEvent failed");
-                inverse_chains(gchains[gi], tp, L);
-            }
-        } else if (pipe && hipEventRecord(pipe->ev[2 * gi + 1], ss) != hipSuccess) {
+        if (pipe && hipEventRecord(pipe->ev[2 * gi + 1], ss) != hipSuccess) {
             return fail_joined(-1, "hipEventRecord failed");
         }
     }
-    if (lanes) { /* every lane and the side stream back into the caller's stream */
-        for (int gi = 0; gi < ngroups; ++gi) {
-            if (hipEventRecord(pipe->ev[EV_LDONE + EV_PER * gi], pipe->lanes[gi]) != hipSuccess ||
-                hipStreamWaitEvent(s, pipe->ev[EV_LDONE + EV_PER * gi], 0) != hipSuccess)
-                return fail(WTP_EHIP, -1, "lane join failed");
-        }
-        if (hipEventRecord(pipe->ev[nev - 1], ss) != hipSuccess || hipStreamWaitEvent(s, pipe->ev[nev - 1], 0) != hipSuccess)
-            return fail(WTP_EHIP, -1, "side-stream join failed");
-    }
     /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2); in
      * the pipelined form group by group, each behind its selection (which joins the side stream) */
-    if (lanes) {
-        /* issued on the lanes above */
-    } else if (pipe) {
+    if (pipe) {
         for (int gi = 0; gi < ngroups; ++gi) {
             if (hipStreamWaitEvent(s, pipe->ev[2 * gi + 1], 0) != hipSuccess) return fail_joined(-1, "hipStreamWaitEvent failed");
             inverse_chains(gchains[gi], tp, s);

@@ -1900,6 +1900,11 @@ __device__ __forceinline__ void res_body(const SegTable& t, const SegDesc& sd, S
         if (!nan) {
             const uint32_t tk = thr > 0.0f ? __float_as_uint(thr) : 1u;
             if (path == MODE_FULL) {
+                /* a selector counts AFTER publishing the granule: in place, the segment's data
+                 * workgroups may already be overwriting sd.data.  The count is unchanged by them:
+                 * where(|x| < thr, 0, x) turns every key < tk into +0 (key 0 < tk) and leaves every
+                 * other key as it was (tests/test_gpu_resident.py::
+                 * test_cfg2_in_place_full_scan_with_selectors) */
                 zc = (unsigned long long)block_count_below<CT>([&](int64_t i) { return abs_key(sd.data[i]); }, sd.n, tk);
             } else {
                 uint32_t c = 0;

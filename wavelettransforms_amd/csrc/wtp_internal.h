@@ -212,7 +212,12 @@ constexpr int RES_PUB_KEYS = (RES_NSUB + 1 + 3) / 4 * 4;
 constexpr int RES_PUB_WORDS = RES_PUB_KEYS + RES_STG * RES_THREADS;
 constexpr int RES_WG_WORDS = RES_PUB_WORDS;
 constexpr int RES_SEL_MAX = 1024;                   /* keys the one-wave select takes (more: full scan) */
-constexpr uint32_t RES_TIMEOUT_DEFAULT_US = 200000; /* a wait this long means the grid is not co-resident */
+/* a wait this long means the grid is not co-resident: 2 ms, about 75x a cfg2 k_resident launch
+ * (26 us) and 60x a cfg3 k_small launch -- every wait inside a co-resident launch ends in a few us.
+ * A grid that is not co-resident (another stream's kernels hold CUs) costs at most this bound plus
+ * the three-launch re-run of its tensors; the round-5 bound was 200 ms (tests/test_gpu_resident.py,
+ * test_two_full_calls_on_two_streams / test_resident_beside_long_kernels measure the cases) */
+constexpr uint32_t RES_TIMEOUT_DEFAULT_US = 2000;
 int resident_capacity();
 /* every resident wait's bound (k_resident, k_small), clamped to RES_TIMEOUT_MAX_US so that the
  * bound in 100 MHz ticks fits 32 bits; returns the previous one */
