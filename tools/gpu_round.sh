@@ -35,6 +35,8 @@ echo "== bench cfg5"; WTP_BENCH_TRACE_DIR="$OUT/trace5_$TAG" timeout -k 10 400 p
 tail -1 "$OUT/bench_cfg5_$TAG.log" | cut -c1-600
 echo "== rehearsal --gpus 2"; WTP_BENCH_REHEARSAL=1 timeout -k 10 300 python bench.py --gpus 2 --steps 40 --warmup 5 > "$OUT/bench_n2_$TAG.log" 2>&1 || { echo rehearsal failed; tail -30 "$OUT/bench_n2_$TAG.log"; exit 1; }
 grep '"metric"' "$OUT/bench_n2_$TAG.log" | cut -c1-400
+echo "== rehearsal --gpus 2 --exchange allgather"; WTP_BENCH_REHEARSAL=1 timeout -k 10 300 python bench.py --gpus 2 --steps 40 --warmup 5 --exchange allgather > "$OUT/bench_n2ag_$TAG.log" 2>&1 || { echo rehearsal allgather failed; tail -30 "$OUT/bench_n2ag_$TAG.log"; exit 1; }
+grep '"metric"' "$OUT/bench_n2ag_$TAG.log" | cut -c1-400
 echo "== rocprof cfg2"; cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 400 --warmup 5 --no-cpu --no-cold --no-rocprof > "$OUT/bench_prof_$TAG.log" 2>&1 || { echo rocprof failed; tail -30 "$OUT/bench_prof_$TAG.log"; exit 1; }
 head -3 "$OUT/prof_$TAG/run_kernel_stats.csv" | cut -c1-200
 echo "== rocprof cfg3"; cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof3_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg3 --steps 400 --warmup 5 --no-cpu --no-cold --no-rocprof > "$OUT/bench_prof3_$TAG.log" 2>&1 || { echo rocprof cfg3 failed; tail -30 "$OUT/bench_prof3_$TAG.log"; exit 1; }

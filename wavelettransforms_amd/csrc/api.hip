@@ -207,7 +207,23 @@ int plan_tensors(const wtp_tensor* ts, int n, int wid, int level, double pct, bo
     return WTP_OK;
 }
 
-Layout make_layout(std::vector<TPlan>& ps) {
+/* Elements one level temp of tensor p needs: the largest intermediate its forward and inverse
+ * write to a temp, level by level, with the kernels forward_chains / inverse_chains pick (tiled:
+ * the next approximation / the synthesis output below level 1; per-point: the column pass's two
+ * outputs / the row pass's two outputs).  Level 1's synthesis writes the caller's output. */
+size_t temp_elems(const TPlan& p, const Taps& tp) {
+    if (p.flat) return (size_t)p.numel + 2; /* two ping-pong lines of up to numel + 1 samples */
+    int64_t need = 0;
+    for (int k = 1; k <= p.L; ++k) {
+        const int64_t R0 = p.g.R[k - 1], C0 = p.g.C[k - 1], R = p.g.R[k], C = p.g.C[k];
+        need = std::max(need, p.B * R * (fb_tiled_ok(p.B, R0, C0, tp) ? C : C0));
+        if (!fb_tiled_ok(p.B, 2 * R, 2 * C, tp)) need = std::max(need, p.B * R * 2 * C);
+        if (k >= 2) need = std::max(need, p.B * 4 * R * C);
+    }
+    return (size_t)need;
+}
+
+Layout make_layout(std::vector<TPlan>& ps, const Taps& tp) {
     Layout L;
     L.hist = 0;
     L.sel = 0;
@@ -231,22 +247,24 @@ Layout make_layout(std::vector<TPlan>& ps) {
         p.p_off = off;
         off = align_up(off + (size_t)p.pop * sizeof(float));
     }
-    /* every tensor has its own level temps: the same level of all tensors runs as one grouped
-     * launch, so their intermediate approximations are live together */
-    for (auto& p : ps) {
-        if (!p.dwt) continue;
-        if (p.flat) { /* two ping-pong lines of up to numel + 1 samples (the last synthesis output) */
-            p.t_elems = (size_t)p.numel + 2;
-            p.t_off = off;
-            off = align_up(off + 3 * align_up(p.t_elems * sizeof(float)));
-            continue;
-        }
-        const int64_t r1 = p.g.R[1], c1 = p.g.C[1];
-        const size_t a = (size_t)(p.B * r1 * (p.W > 2 * c1 ? p.W : 2 * c1));
-        const size_t b = (size_t)(p.B * 2 * r1 * 2 * c1);
-        p.t_elems = std::max(a, b);
-        p.t_off = off;
-        off = align_up(off + 3 * align_up(p.t_elems * sizeof(float)));
+    /* level temps per launch-group SLOT (tensor t uses slot t % SEG_PER_LAUNCH), not per tensor:
+     * the same level of one launch group's tensors runs as one grouped launch, so their temps are
+     * live together, but the groups' transforms run one group after another on the caller's
+     * stream (prune_impl; the side stream only selects from P), so group g + 1 reuses group g's
+     * temps.  cfg5 (64 x 4096^2, db8 L5): 24 slots x 3 x 16.8 MB instead of 64 x 3 x 67 MB */
+    size_t slot_elems[SEG_PER_LAUNCH] = {};
+    for (size_t t = 0; t < ps.size(); ++t)
+        if (ps[t].dwt) slot_elems[t % SEG_PER_LAUNCH] = std::max(slot_elems[t % SEG_PER_LAUNCH], temp_elems(ps[t], tp));
+    size_t slot_off[SEG_PER_LAUNCH] = {};
+    for (int j = 0; j < SEG_PER_LAUNCH; ++j) {
+        if (!slot_elems[j]) continue;
+        slot_off[j] = off;
+        off = align_up(off + 3 * align_up(slot_elems[j] * sizeof(float)));
+    }
+    for (size_t t = 0; t < ps.size(); ++t) {
+        if (!ps[t].dwt) continue;
+        ps[t].t_off = slot_off[t % SEG_PER_LAUNCH];
+        ps[t].t_elems = slot_elems[t % SEG_PER_LAUNCH];
     }
     L.total = off;
     return L;
@@ -578,7 +596,8 @@ size_t wtp_workspace_size(const wtp_tensor* tensors, int ntensors, int wavelet_i
     std::vector<TPlan> ps, pl;
     if (plan_tensors(tensors, ntensors, wavelet_id, level, 50.0, false, ps, true) != WTP_OK) return 0;
     if (plan_tensors(tensors, ntensors, wavelet_id, level, 50.0, false, pl, false) != WTP_OK) return 0;
-    return std::max(make_layout(ps).total, make_layout(pl).total);
+    const Taps tp = (wavelet_id >= 0 && wavelet_id < WT_NUM_WAVELETS) ? make_taps(wavelet_id) : Taps{};
+    return std::max(make_layout(ps, tp).total, make_layout(pl, tp).total);
 }
 
 int wtp_workspace_init(void* ws, size_t bytes, wtp_stream_t stream) {
@@ -631,14 +650,14 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
     std::vector<TPlan> ps;
     int rc = plan_tensors(tensors, ntensors, wavelet_id, level, pct, true, ps, carry, flat);
     if (rc != WTP_OK) return rc;
-    Layout lay = make_layout(ps);
+    const Taps tp = (wavelet_id >= 0 && wavelet_id < WT_NUM_WAVELETS) ? make_taps(wavelet_id) : Taps{};
+    Layout lay = make_layout(ps, tp);
     if (!ws || ws_bytes < lay.total)
         return fail(WTP_EWORKSPACE, -1, "workspace too small: need %zu bytes, got %zu", lay.total, ws_bytes);
     hipStream_t s = (hipStream_t)stream;
     SelHeader* head = reinterpret_cast<SelHeader*>(wsb(ws, lay.sel));
     uint32_t* cand = reinterpret_cast<uint32_t*>(wsb(ws, lay.cand));
     float* thr_t = reinterpret_cast<float*>(wsb(ws, lay.thr));
-    const Taps tp = (wavelet_id >= 0 && wavelet_id < WT_NUM_WAVELETS) ? make_taps(wavelet_id) : Taps{};
 
     stage(0, s);
     if (!no_resident && !flat && g_resident.load(std::memory_order_relaxed)) {
@@ -652,7 +671,6 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         }
     }
     /* 1. forward transforms into the packed arrays (pywt.wavedec2 + coeffs_to_array) */
-    std::vector<Chain> chains;
     const int ngroups = (ntensors + SEG_PER_LAUNCH - 1) / SEG_PER_LAUNCH;
     std::vector<std::vector<Chain>> gchains(ngroups);
     for (int t = 0; t < ntensors; ++t) {
@@ -673,7 +691,6 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             c.T[i] = reinterpret_cast<float*>(wsb(ws, p.t_off + i * align_up(p.t_elems * sizeof(float))));
         c.thr = thr_t + t;
         c.zc = reinterpret_cast<unsigned long long*>(&results[t].zero_count);
-        chains.push_back(c);
         gchains[t / SEG_PER_LAUNCH].push_back(c);
         if (!p.tight && hipMemsetAsync(c.P, 0, (size_t)p.pop * sizeof(float), s) != hipSuccess)
             return fail(WTP_EHIP, t, "hipMemsetAsync failed");
@@ -699,7 +716,8 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         }
         return fail(WTP_EHIP, t, "%s", msg);
     };
-    if (!pipe) forward_chains(chains, tp, s);
+    if (!pipe) /* group by group: the groups share the level temps (make_layout) */
+        for (const auto& gc : gchains) forward_chains(gc, tp, s);
     /* 2. exact percentile selection + level-0 mask, SEG_PER_LAUNCH segments per launch group:
      * one resident launch when every segment of the group is level-0 and the group's chunks fit
      * the co-resident grid, else window / collect / mask-select */
@@ -800,7 +818,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             inverse_chains(gchains[gi], tp, s);
         }
     } else {
-        inverse_chains(chains, tp, s);
+        for (const auto& gc : gchains) inverse_chains(gc, tp, s);
     }
     for (int t = 0; t < ntensors; ++t) {
         const TPlan& p = ps[t];
@@ -830,7 +848,8 @@ size_t wtp_workspace_size_ex(const wtp_tensor* tensors, int ntensors, int wavele
     if (plan_tensors(tensors, ntensors, wavelet_id, level, 50.0, false, ps, (flags & WTP_CARRY_LEVEL) != 0,
                      (flags & WTP_FLATTEN) != 0) != WTP_OK)
         return 0;
-    return make_layout(ps).total;
+    const Taps tp = (wavelet_id >= 0 && wavelet_id < WT_NUM_WAVELETS) ? make_taps(wavelet_id) : Taps{};
+    return make_layout(ps, tp).total;
 }
 
 int wtp_prune_ex_f32(const wtp_tensor* tensors, int ntensors, int wavelet_id, int level, double pct, int flags,
@@ -875,7 +894,7 @@ static int plan_min(const wtp_tensor* ts, int n, double fraction, bool check_ptr
         p.cap = p.numel ? cap_for(p.pop, false) : 0;
         m.nblk += (int)((p.pop + CHUNK - 1) / CHUNK);
     }
-    m.lay = make_layout(m.ps);
+    m.lay = make_layout(m.ps, Taps{}); /* level-0 populations only: no temps */
     m.mp_off = align_up(m.lay.total);
     m.tie_off = align_up(m.mp_off + (size_t)n * 16);
     m.total = align_up(m.tie_off + (size_t)(m.nblk + 1) * sizeof(uint32_t));

@@ -55,6 +55,12 @@ constexpr int FB_MAX_LDS = 64 * 1024;
  * column at FWD_S0 -- so that its column 0 - FWD_S0 is 16-byte aligned in the image (a tile's
  * first input column is 2 FC tc - F/2 + 1) and interior rows load as whole float4s */
 template <int FT> constexpr int FWD_S0 = ((1 - FT / 2) % 4 + 4) % 4;
+/* k_fwd_int's column-pass results in LDS: row o holds its even columns from o * 2 LHH, its odd ones
+ * from o * 2 LHH + LHH (float2 units).  LHH = 8 (mod 16): a wave's float2 writes of consecutive
+ * columns then put the even lanes on banks b .. b + 15 and the odd lanes on b + 16 .. b + 31 of
+ * each 16-lane group (with LHH = (NC + 1) / 2 = 63 at db8 the two halves overlapped on 14 banks:
+ * 0.69 bank-conflict cycles per LDS instruction, round-5 PMC); the row pass reads stay contiguous */
+constexpr int fwd_lhh(int nc) { return (nc + 1) / 2 + ((8 - (nc + 1) / 2) % 16 + 16) % 16; }
 template <int FT> constexpr int FWD_TP = (FWD_S0<FT> + 2 * FC + FT - 2 + 3) / 4 * 4;
 
 
@@ -519,7 +525,8 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int NRc = 2 * FR + FT - 2, NCc = 2 * FC + FT - 2;
     constexpr int S0 = FWD_S0<FT>, TP = FWD_TP<FT>, W4 = TP / 4;
-    constexpr int HALF = (NCc + 1) / 2;
+    constexpr int HALF = fwd_lhh(NCc);
+    static_assert(HALF % 16 == 8 && HALF >= (NCc + 1) / 2, "LH half pitch");
     float* T = lds;
     float2* LH = reinterpret_cast<float2*>(lds);
     const int gt = xcd_tile(blockIdx.x, gridDim.x);
@@ -606,16 +613,19 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
     }
     __syncthreads();
     WTP_FPROBE(1);
-    /* 2. axis -2: one tile column and FR/2 consecutive output rows per item */
+    /* 2. axis -2: one tile column and FR/2 consecutive output rows per item; item it = h HP + cc, with
+     * HP a multiple of 64 when NC fits in 128 (F <= 18): no wave holds items of both halves, whose
+     * column reads 2 RH rows apart would otherwise share LDS banks (round 6, with the LH pitch) */
     constexpr int RH = FR / 2, NV = 2 * RH + FT - 2, NP = NV / 2;
-    constexpr int NIT = (2 * NCc + FB_THREADS - 1) / FB_THREADS;
+    constexpr int HP = NCc <= 128 ? 128 : NCc;
+    constexpr int NIT = (2 * HP + FB_THREADS - 1) / FB_THREADS;
     static_assert(NV % 2 == 0, "sample pairs");
     f2 res[NIT][RH];
 #pragma unroll
     for (int q = 0; q < NIT; ++q) {
         const int it = threadIdx.x + q * FB_THREADS;
-        if (it < 2 * NCc) {
-            const int h = it >= NCc, cc = it - h * NCc;
+        const int h = it >= HP, cc = it - h * HP;
+        if (it < 2 * HP && cc < NCc) {
             const float* col = T + (2 * RH * h) * TP + S0 + cc;
             f2 P[NP];
 #pragma unroll
@@ -648,12 +658,12 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
         }
     }
     __syncthreads(); /* every read of T is done: LH overwrites it */
-    auto lhi = [&](int o, int cc) { return o * NCc + (cc & 1) * HALF + (cc >> 1); };
+    auto lhi = [&](int o, int cc) { return o * (2 * HALF) + (cc & 1) * HALF + (cc >> 1); };
 #pragma unroll
     for (int q = 0; q < NIT; ++q) {
         const int it = threadIdx.x + q * FB_THREADS;
-        if (it < 2 * NCc) {
-            const int h = it >= NCc, cc = it - h * NCc;
+        const int h = it >= HP, cc = it - h * HP;
+        if (it < 2 * HP && cc < NCc) {
 #pragma unroll
             for (int r = 0; r < RH; ++r) LH[lhi(RH * h + r, cc)] = make_float2(res[q][r].x, res[q][r].y);
         }
@@ -1418,7 +1428,9 @@ int fb_set_interior(int mode) { return g_fb_interior.exchange(mode < 0 ? 0 : (mo
  * over their first-pass input (k_fwd_level: LH over T; k_inv_level: LoHi over Aq/Dq) */
 static size_t fwd_lds(int F, bool alias = false) {
     const size_t pitch = alias ? (size_t)(3 + 2 * FC + F - 2 + 3) / 4 * 4 : (size_t)(2 * FC + F - 2); /* >= FWD_TP */
-    const size_t t = (size_t)(2 * FR + F - 2) * pitch, lh = 2 * (size_t)FR * (2 * FC + F - 2);
+    /* lh: k_level's FR x NC float2 rows, or k_fwd_int's FR rows of 2 fwd_lhh(NC) float2 (the larger) */
+    const size_t t = (size_t)(2 * FR + F - 2) * pitch,
+                 lh = 2 * (size_t)FR * std::max<size_t>(2 * FC + F - 2, 2 * (size_t)fwd_lhh(2 * FC + F - 2));
     return sizeof(float) * (alias ? std::max(t, lh) : t + lh);
 }
 static size_t inv_lds(int F, bool alias = false) {
