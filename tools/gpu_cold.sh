@@ -11,6 +11,9 @@ cd /tmp
 echo "== kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 "$ROOT/tools/cold_run.py" --steps 60 > "$OUT/cold_$TAG.log" 2>&1 || { echo trace failed; tail -20 "$OUT/cold_$TAG.log"; exit 1; }
 grep -E "Name|k_resident|Fill" "$OUT/prof_$TAG/run_kernel_stats.csv" | cut -c1-200
+echo "== kernel trace, read flush"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_${TAG}_rd" -o run --output-format csv -- python3 "$ROOT/tools/cold_run.py" --steps 60 --flush read > "$OUT/cold_${TAG}_rd.log" 2>&1 || { echo trace failed; tail -20 "$OUT/cold_${TAG}_rd.log"; exit 1; }
+grep -E "Name|k_resident" "$OUT/prof_${TAG}_rd/run_kernel_stats.csv" | cut -c1-200
 i=0
 for grp in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))

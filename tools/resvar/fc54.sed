@@ -1,0 +1,1 @@
+filterbank.hip	s#constexpr int FR = 16, FC = 56;#constexpr int FR = 16, FC = 54;#

@@ -1433,6 +1433,14 @@ static size_t fwd_lds(int F, bool alias = false) {
                  lh = 2 * (size_t)FR * std::max<size_t>(2 * FC + F - 2, 2 * (size_t)fwd_lhh(2 * FC + F - 2));
     return sizeof(float) * (alias ? std::max(t, lh) : t + lh);
 }
+/* k_fwd_int's exact dynamic LDS: its input tile at pitch FWD_TP (the tile's first column at FWD_S0),
+ * then its column results over it at the fwd_lhh half pitch -- the occupancy is LDS-bound (db8:
+ * 46 x 128 floats = 23 KB, six workgroups per CU) */
+static size_t fwd_int_lds(int F) {
+    const size_t s0 = (size_t)(((1 - F / 2) % 4 + 4) % 4), nc = (size_t)(2 * FC + F - 2);
+    const size_t t = (size_t)(2 * FR + F - 2) * ((s0 + nc + 3) / 4 * 4), lh = 2 * (size_t)FR * 2 * (size_t)fwd_lhh((int)nc);
+    return sizeof(float) * std::max(t, lh);
+}
 static size_t inv_lds(int F, bool alias = false) {
     /* the tile bounds of k_inv_level (IR/2 + H rows, IC/2 + H columns): db8 40 x 40, 25.6 KB aliased --
      * six workgroups per CU instead of five */
@@ -1463,7 +1471,7 @@ static void fwd_int_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t 
     FwdIntTaps t;
     memset(&t, 0, sizeof t);
     for (int j = 0; j < FT; ++j) t.t[j] = f2{tp.f[0][j], tp.f[1][j]};
-    hipLaunchKernelGGL((k_fwd_int<FT, EDGE>), dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, true), s, g, t);
+    hipLaunchKernelGGL((k_fwd_int<FT, EDGE>), dim3(grid), dim3(FB_THREADS), fwd_int_lds(tp.F), s, g, t);
 }
 
 /* The interior rectangle of a forward level's tile grid (k_fwd_int's tiles): a tile row is
