@@ -91,6 +91,23 @@ def test_workspace_size_covers_both_level_modes():
     assert L.wtp_workspace_size(d, 2, wid, 5) >= L.wtp_workspace_size(_desc([(2, 64, 64)]), 1, wid, 5)
 
 
+def test_workspace_footprint_cfg5():
+    """the level temps are sized per level kernel and shared by the launch
+    groups (one set per group slot), so cfg5's workspace (64 x 4096^2, db8 L5) stays under 1.5x its
+    weights (round 5: ~4x), and a call of 24 or fewer tensors still holds its own temps"""
+    L = N.lib()
+    wid = L.wtp_wavelet_id(b"db8")
+    w = 4 * 4096 * 4096
+    big = L.wtp_workspace_size_ex(_desc([(4096, 4096)] * 64), 64, wid, 5, 0)
+    assert 0 < big <= 1.5 * 64 * w, big / (64 * w)
+    one_group = L.wtp_workspace_size_ex(_desc([(4096, 4096)] * 24), 24, wid, 5, 0)
+    # P of every tensor, plus 24 slots of three 2048^2 temps (level 1's approximation)
+    assert one_group >= 24 * w + 24 * 3 * (w // 4)
+    # the 40 extra blocks add their P and candidate buckets (the three-launch selection's, ~12 % of
+    # P), not temps
+    assert 40 * w <= big - one_group < 40 * w * 1.15
+
+
 def test_mode_switches_validate_and_return_the_previous_mode():
     """wtp_set_resident (0 or 1) / wtp_set_pipeline (0 or 1): the previous mode returned,
     anything else rejected with WTP_EARG and the mode left as it was (host logic only, no device
