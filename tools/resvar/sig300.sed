@@ -1,0 +1,1 @@
+wtp_internal.h	s#constexpr int RES_SIGMA_X100 = 400;#constexpr int RES_SIGMA_X100 = 300;#

@@ -627,7 +627,8 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
     uint32_t ka = 0, kb = 0, mk = 0;
     int64_t rem = 0; /* ra inside the rank's 12-bit bin */
     uint32_t d1 = 0, cnt1 = 0;
-    __shared__ uint32_t s_fill, s_min[2];
+    __shared__ uint32_t s_fill, s_min[2], s_lc, s_lk[2];
+    __shared__ uint32_t s_list[64]; /* pass B's keys of digit da (the list form) */
     bool ovf = false;
     uint32_t* G = reinterpret_cast<uint32_t*>(arena + SM_ARENA - SM_GATHER);
     if (ok) {
@@ -698,7 +699,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
             if (i < nw) G[i] = gv[u];
         }
         for (int i = tid; i < 1536; i += SM_THREADS) hist[i] = 0u; /* pass A bins, then pass B's */
-        if (tid == 0) s_min[1] = 0xFFFFFFFFu;
+        if (tid == 0) { s_min[1] = 0xFFFFFFFFu; s_lc = 0u; }
         __syncthreads();
         SM_PROBE(8);
         /* the slot headers (wave 0 reduces them) */
@@ -748,6 +749,39 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
             const uint32_t da = (uint32_t)s_dig[0], db = (uint32_t)s_dig[1];
             const int64_t ra2 = rem - s_bef[0], rb2 = rbi - s_bef[0];
             SM_PROBE(12);
+            /* keys of digit da: hist[da] (the padding zeros included when da == 0) */
+            const uint32_t nda = hist[da];
+            if (nda <= 64u && !(z && da == 0)) { /* block-uniform: the usual case (cfg3: a handful) */
+                /* pass B as a list: the digit's keys appended in LDS, then one wave ranks them by
+                 * counting (rank = keys below + equal keys listed before), instead of a 512-bin
+                 * histogram and a block scan (round 6: k_small 29.1 -> see DESIGN.md) */
+                uint32_t mnA = 0xFFFFFFFFu;
+#pragma unroll
+                for (int u = 0; u < KPT; ++u) {
+                    const uint32_t a = (kk[u] >> 9) & 1023u;
+                    if (kv[u] && a == da) s_list[atomicAdd(&s_lc, 1u)] = kk[u];
+                    else if (kv[u] && a > da) mnA = min(mnA, kk[u]);
+                }
+                mnA = sm_wave_min(mnA);
+                if (lane == 0 && mnA != 0xFFFFFFFFu) atomicMin(&s_min[1], mnA);
+                __syncthreads();
+                if (wv == 0) {
+                    const int n = (int)nda;
+                    const uint32_t mine = lane < n ? s_list[lane] : 0xFFFFFFFFu;
+                    int below = 0;
+                    for (int j = 0; j < n; ++j) {
+                        const uint32_t kj = s_list[j];
+                        below += (kj < mine) | ((kj == mine) & (j < lane));
+                    }
+                    if (lane < n && below == (int)ra2) s_lk[0] = mine;
+                    if (lane < n && below == (int)rb2) s_lk[1] = mine;
+                }
+                __syncthreads();
+                ka = s_lk[0];
+                if (rbi >= (int64_t)cnt1) kb = mnab;             /* rb past the bin: the next key above it */
+                else if (rb2 >= (int64_t)nda) kb = s_min[1];     /* rb in a later 10-bit group of the bin */
+                else kb = s_lk[1];
+            } else {
             uint32_t* hb = hist + 1024;
             uint32_t mnA = 0xFFFFFFFFu;
 #pragma unroll
@@ -765,6 +799,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_small(SmallTable t, SelHeader* _
             if (rbi >= (int64_t)cnt1) kb = mnab;             /* rb past the bin: the next key above it */
             else if (db != da) kb = s_min[1];                /* rb in a later 10-bit group of the bin */
             else kb = (d1 << 19) | (da << 9) | (uint32_t)s_dig[1];
+            }
         }
         SM_PROBE(13);
     }
