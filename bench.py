@@ -78,6 +78,9 @@ def parse():
                     help="run the frame of edge tiles in the general kernel (wtp_set_interior(1); A/B only)")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="wtp_set_pipeline mode for multi-group calls (default: the library's; A/B only)")
+    ap.add_argument("--no-fused-select", action="store_true",
+                    help="cfg5-sized groups: the window / collect / select passes over the packed array instead of "
+                         "the fused selection (wtp_set_fused_select(0); A/B only)")
     ap.add_argument("--frame-apart", action="store_true",
                     help="the frame of edge tiles in a launch of its own (wtp_set_interior(2); A/B only)")
     ap.add_argument("--no-rocprof", action="store_true", help="skip the in-run rocprofv3 kernel-stats child")
@@ -146,6 +149,8 @@ def rocprof_child(args, timeout=240):
         cmd.append("--frame-apart")
     if args.pipeline is not None:
         cmd += ["--pipeline", str(args.pipeline)]
+    if args.no_fused_select:
+        cmd.append("--no-fused-select")
     env = dict(os.environ, TMPDIR="/tmp")
     try:
         subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
@@ -276,6 +281,8 @@ def main():
         engine.set_interior(2)
     if args.pipeline is not None:
         engine.set_pipeline(args.pipeline)
+    if args.no_fused_select:
+        engine.set_fused_select(False)
 
     # ---------------------------------------------------------------- workload
     if args.config == "cfg2":

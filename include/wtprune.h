@@ -187,6 +187,14 @@ unsigned wtp_set_resident_timeout_us(unsigned us);
  * the caller's stream (graph capture included).  Mode 0: everything on the caller's stream; any
  * other value is rejected (WTP_EARG).  Returns the previous mode (process-wide). */
 int wtp_set_pipeline(int mode);
+/* Fused selection for launch groups of large wavelet-transformed tensors (each >= 2^22 packed
+ * coefficients, every forward level in the tiled interior kernels, at most 6 levels, images of at
+ * least 128 x 128): the percentile window comes from a transform of four 128 x 128 input patches
+ * before the forward, the forward classifies the coefficients as it writes them, and the packed
+ * array is not read again for the selection (identical results: a window that misses the ranks is
+ * caught by the select, which then takes its exact full scan).  Mode 1 (default) on, 0 off; any
+ * other value is rejected (WTP_EARG).  Returns the previous mode (process-wide). */
+int wtp_set_fused_select(int mode);
 /* The filter-bank levels run their interior tiles (input window inside the image, full tile)
  * in kernels compiled without the edge forms and the frame of edge tiles in the same kernels'
  * edge-capable form (mode 2); mode 3 (default) as 2, but a small level (a few thousand tiles)

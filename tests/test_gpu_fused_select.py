@@ -1,0 +1,173 @@
+"""Fused selection (include/wtprune.h wtp_set_fused_select; csrc/kernels.hip k_fwin /
+k_fslot_collect, csrc/filterbank.hip k_fwd_int's classification): launch groups of large
+wavelet-transformed tensors take their percentile window from a transform of input patches
+before the forward, the forward classifies the coefficients as it writes them, and the packed
+array is never re-read for the selection.  The results must equal the unfused form (window /
+collect / select over the packed array) and the C oracle bit for bit (values, float64 threshold
+bits, zero counts) -- out of place, in place, inside a captured graph, beside unfused groups of
+the same call -- and a window that misses (patches unrepresentative of the tensor) must end in the
+exact full-scan select with the same results.  Reference path: dwt_pruning.py:53-89 per tensor."""
+import math
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests import golden_io as G
+
+pytestmark = pytest.mark.gpu
+
+MODE_CAND, MODE_FULL = 1, 3
+# each >= 2^22 packed coefficients, tight (dims divisible by 2^L), images >= 128 x 128, and at
+# level <= 4 every forward level of these images has interior tiles (k_fwd_int throughout)
+SHAPES = [(2048, 2048), (2, 1024, 2048), (1, 2048, 3072)]
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from wavelettransforms_amd import engine
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    prev = engine.set_fused_select(True)
+    yield engine
+    engine.set_fused_select(prev)
+
+
+def _e(shape, i):
+    """weight-sized values (block_tensors' exponent: sigma ~ sqrt(2 / side)), varied per tensor --
+    inside the window bins' range [2^-26, 2^6), as every real layer is"""
+    return G.W.sigma_exponent(math.sqrt(2.0 / shape[-1])) + i % 3
+
+
+def _inputs(eng, shapes=SHAPES, seed=11):
+    return [eng.synth(s, seed, i, _e(s, i)) for i, s in enumerate(shapes)]
+
+
+def _run(eng, xs, fused, wavelet, level, pct, in_place=False):
+    prev = eng.set_fused_select(fused)
+    try:
+        outs = [x.clone() for x in xs] if in_place else None
+        o, r = eng.prune(outs if in_place else xs, wavelet, level, pct, outs=outs, carry_level=False)
+        torch.cuda.synchronize()
+        return [t.cpu().numpy() for t in o], r
+    finally:
+        eng.set_fused_select(prev)
+
+
+def _same(a, b):
+    (oa, ra), (ob, rb) = a, b
+    assert len(oa) == len(ob)
+    for x, y, p, q in zip(oa, ob, ra, rb):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+        assert p["zero_count"] == q["zero_count"] and p["eff_level"] == q["eff_level"]
+        assert G.f64_bits_equal(p["thr64"], q["thr64"])
+        assert int(p["thr32_bits"]) == int(q["thr32_bits"]) and int(p["max_abs_bits"]) == int(q["max_abs_bits"])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("wavelet,level,pct", [("db8", 4, 50.0), ("bior3.3", 4, 75.0), ("haar", 3, 30.0)])
+def test_fused_equals_unfused_and_oracle(eng, wavelet, level, pct):
+    xs = _inputs(eng)
+    a = _run(eng, xs, True, wavelet, level, pct)
+    _same(a, _run(eng, xs, False, wavelet, level, pct))
+    # the window came from the patches and held the ranks (no full scan)
+    assert all(r["path"] == MODE_CAND for r in a[1]), [r["path"] for r in a[1]]
+    for i, s in enumerate(SHAPES):
+        ref, rr = O.prune_tensor(G.W.synth_numpy(s, 11, i, _e(s, i)), wavelet, level, pct)
+        assert np.array_equal(a[0][i].view(np.uint32), ref.view(np.uint32)), i
+        assert a[1][i]["zero_count"] == rr["zero_count"]
+        assert G.f64_bits_equal(a[1][i]["thr64"], rr["thr64"])
+
+
+@pytest.mark.timeout(300)
+def test_fused_in_place(eng):
+    xs = _inputs(eng)
+    _same(_run(eng, xs, True, "db8", 4, 50.0, in_place=True), _run(eng, xs, False, "db8", 4, 50.0))
+
+
+def _patch_origins(R, C):
+    """k_fwin's patch origins (csrc/kernels.hip): rows at 1/8, 3/8, 5/8, 7/8 and columns at 3/8,
+    7/8, 1/8, 5/8 of the free range, FWIN_PS = 128"""
+    return [((R - 128) * lr // 8, (C - 128) * lc // 8) for lr, lc in zip((1, 3, 5, 7), (3, 7, 1, 5))]
+
+
+@pytest.mark.timeout(300)
+def test_window_miss_takes_the_exact_full_scan(eng):
+    """Everything outside the four patches scaled by 16: the patches' window sits far below the
+    tensor's percentile, the select sees the ranks above it and scans the packed array in full;
+    the unfused form (its window sampled from the packed array itself) holds the ranks.  Same
+    results either way, and equal to the oracle."""
+    R, C = 2048, 2048
+    x = eng.synth((R, C), 5, 0, _e((R, C), 0))
+    scale = torch.full((R, C), 16.0, device=x.device)
+    for r0, c0 in _patch_origins(R, C):
+        scale[r0:r0 + 128, c0:c0 + 128] = 1.0
+    x = x * scale
+    a = _run(eng, [x], True, "db8", 4, 50.0)
+    b = _run(eng, [x], False, "db8", 4, 50.0)
+    _same(a, b)
+    assert a[1][0]["path"] == MODE_FULL and b[1][0]["path"] == MODE_CAND, (a[1][0]["path"], b[1][0]["path"])
+    ref, rr = O.prune_tensor(x.cpu().numpy(), "db8", 4, 50.0)
+    assert np.array_equal(a[0][0].view(np.uint32), ref.view(np.uint32))
+    assert G.f64_bits_equal(a[1][0]["thr64"], rr["thr64"])
+
+
+@pytest.mark.timeout(300)
+def test_heavy_ties(eng):
+    """Integer-valued input in {-2..2}: the haar coefficients take a handful of values, so the
+    window's bins hold many equal keys (slot overflow and bucket overflow send the select to its
+    full scan); the results still equal the unfused form and the oracle."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    xn = torch.randint(-2, 3, (2048, 2048), generator=g).float()
+    x = xn.cuda()
+    for pct in (50.0, 90.0):
+        a = _run(eng, [x], True, "haar", 3, pct)
+        _same(a, _run(eng, [x], False, "haar", 3, pct))
+        ref, rr = O.prune_tensor(xn.numpy(), "haar", 3, pct)
+        assert np.array_equal(a[0][0].view(np.uint32), ref.view(np.uint32))
+        assert a[1][0]["zero_count"] == rr["zero_count"]
+
+
+@pytest.mark.timeout(300)
+def test_fused_and_unfused_groups_in_one_call(eng):
+    """26 tensors: a first launch group of 24 large tensors (fused), then a group of one large and
+    one small tensor (the small one does not qualify, so that group runs unfused); the SelState
+    parity regions alternate over both kinds of group."""
+    shapes = [(1024, 4096)] * 24 + [(2048, 2048), (3, 64, 64)]
+    xs = _inputs(eng, shapes, seed=2)
+    a = _run(eng, xs, True, "db8", 4, 50.0)
+    _same(a, _run(eng, xs, False, "db8", 4, 50.0))
+    assert all(r["path"] == MODE_CAND for r in a[1][:24])
+    for i in (0, 23, 24, 25):
+        ref, rr = O.prune_tensor(G.W.synth_numpy(shapes[i], 2, i, _e(shapes[i], i)), "db8", 4, 50.0)
+        assert np.array_equal(a[0][i].view(np.uint32), ref.view(np.uint32)), i
+        assert G.f64_bits_equal(a[1][i]["thr64"], rr["thr64"])
+
+
+@pytest.mark.timeout(300)
+def test_fused_graph_capture_and_replay(eng):
+    """bench.py captures its steps: two fused calls of two launch groups each (the second group's
+    forward beside the first group's bucket pass and select on the side stream) in one capture
+    replay to the eager results."""
+    xs = _inputs(eng, [(1024, 4096)] * 25, seed=4)
+    ref = _run(eng, xs, True, "db8", 4, 50.0)
+    outs = [torch.empty_like(x) for x in xs]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm-up: the workspace exists before the capture
+        eng.launch(xs, "db8", 4, 50.0, outs=outs, carry_level=False, stream=s)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(2):
+                _, resd = eng.launch(xs, "db8", 4, 50.0, outs=outs, carry_level=False)
+    for o in outs:
+        o.zero_()
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    _same(([o.cpu().numpy() for o in outs], eng.decode(resd, len(xs))), ref)

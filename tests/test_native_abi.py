@@ -104,16 +104,17 @@ def test_workspace_footprint_cfg5():
     # P of every tensor, plus 24 slots of three 2048^2 temps (level 1's approximation)
     assert one_group >= 24 * w + 24 * 3 * (w // 4)
     # the 40 extra blocks add their P and candidate buckets (the three-launch selection's, ~12 % of
-    # P), not temps
-    assert 40 * w <= big - one_group < 40 * w * 1.15
+    # P), not temps; with more than one group the fused selection's slot areas come in two sets
+    # (24 x ~6.5 MB more)
+    assert 40 * w <= big - one_group < 40 * w * 1.2
 
 
 def test_mode_switches_validate_and_return_the_previous_mode():
-    """wtp_set_resident (0 or 1) / wtp_set_pipeline (0 or 1): the previous mode returned,
+    """wtp_set_resident / wtp_set_pipeline / wtp_set_fused_select (0 or 1): the previous mode returned,
     anything else rejected with WTP_EARG and the mode left as it was (host logic only, no device
     work)."""
     L = N.lib()
-    for setter, top in ((L.wtp_set_resident, 1), (L.wtp_set_pipeline, 1)):
+    for setter, top in ((L.wtp_set_resident, 1), (L.wtp_set_pipeline, 1), (L.wtp_set_fused_select, 1)):
         prev = setter(0)
         assert prev in range(top + 1)
         assert setter(1) == 0

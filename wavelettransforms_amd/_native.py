@@ -81,6 +81,7 @@ def lib():
             "wtp_count_small_f32": ([vp, i64, ctypes.c_float, vp, vp], i32),
             "wtp_set_resident": ([i32], i32),
             "wtp_set_pipeline": ([i32], i32),
+            "wtp_set_fused_select": ([i32], i32),
             "wtp_set_interior": ([i32], i32),
             "wtp_resident_capacity": ([], i32),
             "wtp_set_resident_timeout_us": ([ctypes.c_uint], ctypes.c_uint),

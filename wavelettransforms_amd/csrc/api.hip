@@ -30,6 +30,7 @@ thread_local hipEvent_t g_stage_ev[8];
 thread_local int g_stage_n = 0;
 std::atomic<int> g_resident{1}; /* wtp_set_resident */
 std::atomic<int> g_pipeline{1}; /* wtp_set_pipeline */
+std::atomic<int> g_fused{1};    /* wtp_set_fused_select */
 
 inline void stage(int i, hipStream_t s) {
     if (i < g_stage_n && g_stage_ev[i]) (void)hipEventRecord(g_stage_ev[i], s);
@@ -87,6 +88,8 @@ struct TPlan {
     size_t t_off = 0;     /* workspace byte offset of this tensor's three level temps      */
     size_t t_elems = 0;   /* elements per temp                                              */
     bool flat = false;    /* 1-D flattened mode: pywt.wavedec / waverec of the flat tensor   */
+    int64_t f_slots = 0;  /* fused selection: k_fwd_int wave slots of its forward (0: never fused) */
+    size_t f_off = 0;     /* workspace byte offset of its slot area (per group parity and slot) */
     int64_t len[34] = {}; /* flat: len[0] = numel, len[k] = ceil(len[k-1] / 2)              */
 };
 
@@ -95,7 +98,7 @@ struct Layout {
 };
 
 /* persistent slot region: identical position and size in every layout */
-constexpr size_t PERSIST_BYTES = ((sizeof(SelHeader) + 2 * SEL_REGION) + 255) / 256 * 256;
+constexpr size_t PERSIST_BYTES = ((sizeof(SelHeader) + 2 * SEL_REGION + FWIN_HIST_BYTES) + 255) / 256 * 256;
 
 bool pct_ok(double pct) { return pct >= 0.0 && pct <= 100.0; }
 
@@ -223,6 +226,30 @@ size_t temp_elems(const TPlan& p, const Taps& tp) {
     return (size_t)need;
 }
 
+/* Fused selection (wtp_internal.h, FwdSel / k_fwin / k_fslot_collect): a tensor qualifies when
+ * it is large (its window pass and bucket pass are then small beside the P re-read they replace),
+ * tight (every packed coefficient is written by the forward: no padding zeros in the population),
+ * its images hold k_fwin's patches and its level count leaves them at least 4 x 4, and every
+ * forward level runs in k_fwd_int.  Returns the wave slots of its forward, 0 when it does not
+ * qualify.  `sizing`: the workspace query -- the interior mode and the input's alignment are
+ * not known yet, so the slots are reserved whenever the shape qualifies. */
+constexpr int64_t FUSED_MIN_POP = (int64_t)1 << 22;
+int64_t fused_slot_count(const TPlan& p, const float* in, const Taps& tp, bool sizing) {
+    if (!p.dwt || p.flat || !p.tight || p.L < 1 || p.L > 6 || p.pop < FUSED_MIN_POP) return 0;
+    if (p.g.R[0] < FWIN_PS || p.g.C[0] < FWIN_PS) return 0;
+    int64_t tot = 0;
+    for (int k = 1; k <= p.L; ++k) {
+        /* level 1 reads the caller's input, the others a 256-byte aligned temp */
+        const float* src = (k == 1 && !sizing) ? in : reinterpret_cast<const float*>((uintptr_t)ALIGN);
+        const FwdItem x{src, p.B, p.g.R[k - 1], p.g.C[k - 1], nullptr, nullptr, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k],
+                        k == p.L};
+        int64_t sl = 0;
+        if (!fwd_level_fused_ok(x, tp, &sl, sizing)) return 0;
+        tot += sl;
+    }
+    return tot;
+}
+
 Layout make_layout(std::vector<TPlan>& ps, const Taps& tp) {
     Layout L;
     L.hist = 0;
@@ -266,6 +293,27 @@ Layout make_layout(std::vector<TPlan>& ps, const Taps& tp) {
         ps[t].t_off = slot_off[t % SEG_PER_LAUNCH];
         ps[t].t_elems = slot_elems[t % SEG_PER_LAUNCH];
     }
+    /* fused selection's wave slots, also per launch-group slot: a fused group's bucket pass reads
+     * them before the next group's forward writes its own */
+    size_t fsl_words[SEG_PER_LAUNCH] = {};
+    for (size_t t = 0; t < ps.size(); ++t) {
+        ps[t].f_slots = fused_slot_count(ps[t], nullptr, tp, true);
+        if (ps[t].f_slots)
+            fsl_words[t % SEG_PER_LAUNCH] =
+                std::max(fsl_words[t % SEG_PER_LAUNCH], (size_t)FSL_HDR_WORDS + (size_t)ps[t].f_slots * FSL_WORDS);
+    }
+    /* two sets when the call has several groups: group g uses set g & 1, so group g + 1's forward
+     * fills its slots while group g's bucket pass (side stream) still reads its own */
+    const int nsets = ps.size() > (size_t)SEG_PER_LAUNCH ? 2 : 1;
+    size_t fsl_off[2][SEG_PER_LAUNCH] = {};
+    for (int k = 0; k < nsets; ++k)
+        for (int j = 0; j < SEG_PER_LAUNCH; ++j) {
+            if (!fsl_words[j]) continue;
+            fsl_off[k][j] = off;
+            off = align_up(off + fsl_words[j] * sizeof(uint32_t));
+        }
+    for (size_t t = 0; t < ps.size(); ++t)
+        if (ps[t].f_slots) ps[t].f_off = fsl_off[(t / SEG_PER_LAUNCH) & 1][t % SEG_PER_LAUNCH];
     L.total = off;
     return L;
 }
@@ -304,17 +352,20 @@ struct Chain {
     float* T[3];
     const float* thr;
     unsigned long long* zc;
+    uint32_t* fsl = nullptr; /* fused selection: the tensor's slot area (null: not fused) */
 };
 
 /* pywt.wavedec2 (dwt_pruning.py:67-68) of every chain into its packed layout.  Level k of all
  * chains is ONE tiled launch (filterbank.hip) where the level is large enough, else the two
  * per-point passes of that chain.  Each approximation ping-pongs between the chain's own temps
  * so no launch reads what it writes. */
-void forward_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s) {
+void forward_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s, bool fused = false) {
     int maxL = 0;
     for (const Chain& c : cs) maxL = std::max(maxL, c.p->L);
     std::vector<const float*> cur(cs.size());
     for (size_t j = 0; j < cs.size(); ++j) cur[j] = cs[j].in;
+    std::vector<uint32_t*> fcur(cs.size()); /* fused selection: each chain's next level's slots */
+    for (size_t j = 0; j < cs.size(); ++j) fcur[j] = (fused && cs[j].fsl) ? cs[j].fsl + FSL_HDR_WORDS : nullptr;
     std::vector<FwdItem> items;
     for (int k = 1; k <= maxL; ++k) {
         items.clear();
@@ -327,6 +378,12 @@ void forward_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s)
                 float* an = (cur[j] == tA) ? tL : tA;
                 items.push_back(FwdItem{cur[j], p.B, R0, C0, an, cs[j].P, p.g.PR, p.g.PC, p.g.offR[k], p.g.offC[k],
                                         k == p.L});
+                int64_t sl = 0;
+                if (fcur[j] && fwd_level_fused_ok(items.back(), tp, &sl)) { /* prune_impl checked every level */
+                    items.back().fslot = fcur[j];
+                    items.back().fhdr = reinterpret_cast<FslHeader*>(cs[j].fsl);
+                    fcur[j] += sl * FSL_WORDS;
+                }
                 cur[j] = an;
             } else {
                 float* t0 = (cur[j] == tL) ? tA : tL;
@@ -338,7 +395,7 @@ void forward_chains(const std::vector<Chain>& cs, const Taps& tp, hipStream_t s)
                 cur[j] = an;
             }
         }
-        if (!items.empty()) launch_fwd_levels(items.data(), (int)items.size(), tp, s);
+        if (!items.empty()) launch_fwd_levels(items.data(), (int)items.size(), tp, s, fused);
     }
 }
 
@@ -584,6 +641,10 @@ int wtp_set_pipeline(int mode) {
     if (mode < 0 || mode > 1) return fail(WTP_EARG, -1, "bad pipeline mode %d", mode);
     return g_pipeline.exchange(mode);
 }
+int wtp_set_fused_select(int mode) {
+    if (mode < 0 || mode > 1) return fail(WTP_EARG, -1, "bad fused-select mode %d", mode);
+    return g_fused.exchange(mode);
+}
 unsigned wtp_set_resident_timeout_us(unsigned us) { return set_resident_timeout_us(us); }
 int wtp_set_kernel_stamps(unsigned long long* stamps_dev) {
     set_kernel_stamps(stamps_dev);
@@ -691,12 +752,28 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             c.T[i] = reinterpret_cast<float*>(wsb(ws, p.t_off + i * align_up(p.t_elems * sizeof(float))));
         c.thr = thr_t + t;
         c.zc = reinterpret_cast<unsigned long long*>(&results[t].zero_count);
+        if (p.f_slots) c.fsl = reinterpret_cast<uint32_t*>(wsb(ws, p.f_off));
         gchains[t / SEG_PER_LAUNCH].push_back(c);
         if (!p.tight && hipMemsetAsync(c.P, 0, (size_t)p.pop * sizeof(float), s) != hipSuccess)
             return fail(WTP_EHIP, t, "hipMemsetAsync failed");
     }
     int dwt_groups = 0;
     for (const auto& gc : gchains) dwt_groups += !gc.empty();
+    /* fused selection per launch group: every tensor of the group qualifies with its real input
+     * pointer and the current interior mode (fused_slot_count) */
+    std::vector<char> fused(ngroups, 0);
+    bool any_fused = false;
+    if (g_fused.load(std::memory_order_relaxed)) {
+        for (int gi = 0; gi < ngroups; ++gi) {
+            const int g0 = gi * SEG_PER_LAUNCH, g1 = std::min(ntensors, g0 + SEG_PER_LAUNCH);
+            bool ok = true;
+            for (int t = g0; t < g1 && ok; ++t)
+                ok = ps[t].f_slots > 0 && fused_slot_count(ps[t], tensors[t].in, tp, false) == ps[t].f_slots;
+            fused[gi] = ok;
+            any_fused = any_fused || ok;
+        }
+    }
+    (void)any_fused;
     const int pmode = dwt_groups > 1 ? g_pipeline.load(std::memory_order_relaxed) : 0;
     /* events 2g (group g's forward done) and 2g + 1 (its selection done); the last one joins the
      * side stream back on an error path.  (Round 5's mode 2 -- each group's levels on a lane
@@ -716,29 +793,25 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         }
         return fail(WTP_EHIP, t, "%s", msg);
     };
-    if (!pipe) /* group by group: the groups share the level temps (make_layout) */
-        for (const auto& gc : gchains) forward_chains(gc, tp, s);
+    if (!pipe) /* group by group: the groups share the level temps (make_layout); a fused group's
+                * forward runs behind its window pass, in the selection loop below */
+        for (int gi = 0; gi < ngroups; ++gi)
+            if (!fused[gi]) forward_chains(gchains[gi], tp, s);
     /* 2. exact percentile selection + level-0 mask, SEG_PER_LAUNCH segments per launch group:
      * one resident launch when every segment of the group is level-0 and the group's chunks fit
      * the co-resident grid, else window / collect / mask-select */
     for (int g0 = 0; g0 < ntensors; g0 += SEG_PER_LAUNCH) {
         const int g1 = std::min(ntensors, g0 + SEG_PER_LAUNCH);
         const int gi = g0 / SEG_PER_LAUNCH;
-        if (pipe) { /* this group's forward levels on the caller's stream, its selection behind them */
-            forward_chains(gchains[gi], tp, s);
-            if (hipEventRecord(pipe->ev[2 * gi], s) != hipSuccess) return fail_joined(-1, "hipEventRecord failed");
-            if (hipStreamWaitEvent(ss, pipe->ev[2 * gi], 0) != hipSuccess)
-                return fail_joined(-1, "hipStreamWaitEvent failed");
-            forked = true;
-        }
         bool all0 = true;
         int64_t rblk = 0;
         for (int t = g0; t < g1; ++t) {
             all0 = all0 && !ps[t].dwt;
             rblk += (ps[t].pop + RES_CHUNK - 1) / RES_CHUNK;
         }
-        const bool resident = all0 && !no_resident && g_resident.load(std::memory_order_relaxed) && rblk <= RES_MAX_WG &&
-                              rblk <= resident_capacity();
+        const bool fz = fused[gi] != 0;
+        const bool resident = !fz && all0 && !no_resident && g_resident.load(std::memory_order_relaxed) &&
+                              rblk <= RES_MAX_WG && rblk <= resident_capacity();
         const int64_t chunk = resident ? RES_CHUNK : CHUNK;
         SegTable tab;
         memset(&tab, 0, sizeof tab);
@@ -786,16 +859,69 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
                                      (uint64_t)(RES_MS / SAMPLE_GROUP - 1);
             }
             if (late[t - g0]) sd.flags |= SEG_LATE;
-            blk += (int)((p.pop + chunk - 1) / chunk);
+            if (fz) { /* k_fslot_collect: one block per FSC_SLOTS wave slots */
+                sd.fsl = reinterpret_cast<const uint32_t*>(wsb(ws, p.f_off));
+                sd.fsl_n = (int32_t)p.f_slots;
+                blk += (int)((p.f_slots + FSC_SLOTS - 1) / FSC_SLOTS);
+            } else {
+                blk += (int)((p.pop + chunk - 1) / chunk);
+            }
         }
         tab.nblk = blk;
         for (int i = tab.nseg; i < SEG_PER_LAUNCH; ++i) tab.blk_begin[i] = INT32_MAX;
         const bool first = g0 == 0;
-        if (first) stage(1, ss);
-        if (resident) {
+        FwinTable ft;
+        if (fz) {
+            /* fused: the window from the input's patches (into each tensor's slot-area head), the
+             * forward classifying what it writes; then the bucket pass over its slots and the
+             * select, on the side stream when the call is pipelined */
+            memset(&ft, 0, sizeof ft);
+            ft.nseg = tab.nseg;
+            ft.F = tp.F;
+            ft.gh = fwin_hist(head);
+            for (int j = 0; j < tp.F && j < FWIN_F_MAX; ++j) { ft.lo[j] = tp.f[0][j]; ft.hi[j] = tp.f[1][j]; }
+            for (int i = 0; i < tab.nseg; ++i) {
+                const TPlan& p = ps[g0 + i];
+                FwinSeg& f = ft.s[i];
+                f.in = tensors[g0 + i].in;
+                f.hdr = reinterpret_cast<FslHeader*>(wsb(ws, p.f_off));
+                f.n = tab.s[i].n;
+                f.r0 = tab.s[i].r0;
+                f.above = tab.s[i].above;
+                f.nsub_log2 = tab.s[i].nsub_log2;
+                f.B = (int32_t)p.B;
+                f.R = (int32_t)p.g.R[0];
+                f.C = (int32_t)p.g.C[0];
+                f.L = p.L;
+            }
+        }
+        if (pipe) { /* this group's forward levels on the caller's stream, its selection behind them */
+            if (fz) {
+                /* group gi - 2 used the same slot areas: its bucket pass has read them */
+                if (gi >= 2 && hipStreamWaitEvent(s, pipe->ev[2 * (gi - 2) + 1], 0) != hipSuccess)
+                    return fail_joined(-1, "hipStreamWaitEvent failed");
+                launch_fwin(ft, head, s);
+            }
+            forward_chains(gchains[gi], tp, s, fz);
+            if (hipEventRecord(pipe->ev[2 * gi], s) != hipSuccess) return fail_joined(-1, "hipEventRecord failed");
+            if (hipStreamWaitEvent(ss, pipe->ev[2 * gi], 0) != hipSuccess)
+                return fail_joined(-1, "hipStreamWaitEvent failed");
+            forked = true;
+        } else if (fz) {
+            launch_fwin(ft, head, s);
+            forward_chains(gchains[gi], tp, s, true);
+        }
+        if (fz) {
+            if (first) { stage(1, ss); stage(2, ss); }
+            launch_fslot_collect(tab, head, cand, results, ss);
+            if (first) stage(3, ss);
+            launch_mask_select(tab, head, cand, results, thr_t, ss);
+        } else if (resident) {
+            if (first) stage(1, ss);
             if (first) { stage(2, ss); stage(3, ss); }
             launch_resident(tab, head, cand, results, thr_t, ss);
         } else {
+            if (first) stage(1, ss);
             launch_window(tab, head, ss);
             if (first) stage(2, ss);
             launch_collect(tab, head, cand, results, ss);

@@ -520,7 +520,7 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_FWD_WPE void k_fwd_level(FwdGrou
  *   row pass: as k_fwd_level's interior form; stores by buffer instructions whose row offset is a
  *   scalar (the row is wave-uniform) and column offset the lane's -- no 64-bit address math. */
 template <int FT, bool EDGE>
-__global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup g, FwdIntTaps tp) {
+__global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup g, FwdIntTaps tp, FwdSel fs) {
     static_assert(FT > 0 && FT % 2 == 0, "specialised even filters");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int NRc = 2 * FR + FT - 2, NCc = 2 * FC + FT - 2;
@@ -549,6 +549,18 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
     const int gr0 = 2 * o0r - FT / 2 + 1, gc0 = 2 * o0c - FT / 2 + 1;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const float* x = g.in[item] + (int64_t)b * a.in_bs;
+    /* fused selection (FwdSel): the window of the item's segment, by scalar loads in flight with
+     * the tile's, and the wave's slot */
+    const bool fsel = fs.on != 0;
+    uint32_t skl = 0, sspan = 0;
+    FslHeader* sst = nullptr;
+    uint32_t* wslot = nullptr;
+    if (fsel) {
+        sst = fs.hdr[item];
+        skl = sst->kl;
+        sspan = sst->kh - skl;
+        wslot = fs.slots[item] + ((int64_t)tile * (FB_THREADS / 64) + wv) * FSL_WORDS;
+    }
     WTP_FPROBE(0);
     /* 1. the input tile; every load of a thread in flight before its first LDS write */
     if (EDGE && a.al16 && !(a.R & 1) && a.R >= NRc && a.C >= TP) {
@@ -682,6 +694,25 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
         const int ic = FT / 2 + 2 * (o0c + lane);
         fxm = __ballot(lane < FC && ic >= a.C && o0c + lane < a.Co);
     }
+    /* fused selection: every coefficient the wave writes to P is classified against the window
+     * [kl, kh] as k_collect classifies a chunk: keys < kl and == kl counted (ballot popcounts), the
+     * largest key kept, the keys inside (kl, kh] appended to the wave's slot in write order.  Every
+     * lane of the row pass takes every call (ok = the output exists), so the running count stays
+     * the same in all of them. */
+    uint32_t f_below = 0, f_eq = 0, f_cnt = 0, f_mx = 0;
+    auto fcls = [&](float v, bool ok) {
+        const uint32_t k = __float_as_uint(v) & 0x7FFFFFFFu;
+        f_below += (uint32_t)__popcll(__ballot(ok && k < skl));
+        f_eq += (uint32_t)__popcll(__ballot(ok && k == skl));
+        f_mx = (ok && k > f_mx) ? k : f_mx;
+        const bool in = ok && k - skl - 1u < sspan;
+        const uint64_t m = __ballot(in);
+        if (m) {
+            const uint32_t pos = f_cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (in && pos < (uint32_t)FSL_KEYS) wslot[1 + pos] = k;
+            f_cnt += (uint32_t)__popcll(m);
+        }
+    };
     if (lane < FC) {
         const __amdgpu_buffer_rsrc_t rP =
             __builtin_amdgcn_make_buffer_rsrc(g.P[item] + (int64_t)b * a.P_bs, 0, (int)(4 * a.P_bs), 0x00020000);
@@ -719,8 +750,15 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const int r = o0r + (u ? oB : oA);
-                if (EDGE && !(cin && r < a.Ro)) continue;
+                const bool ok = !EDGE || (cin && r < a.Ro);
                 const f2 lw = u ? aB : aA, hg = u ? dB : dA;
+                if (fsel) {
+                    fcls(hg.x, ok);
+                    fcls(lw.y, ok);
+                    fcls(hg.y, ok);
+                    if (a.last) fcls(lw.x, ok);
+                }
+                if (!ok) continue;
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.x), rA, voff, 4 * r * pitchA, 0);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.x), rP, voff, 4 * (r * a.PC + a.offC), 0);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.y), rP, voff, 4 * ((a.offR + r) * a.PC), 0);
@@ -730,7 +768,8 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
     }
     if (EDGE && fxm) { /* uniform */
         const int nsc = __builtin_popcountll(fxm);
-        static_assert(2 * NPR * (FT / 4 + 2) <= 64, "one fix-up pass per wave");
+        /* the fix-up lanes are row-pass lanes (lane < FC): their running slot count is current */
+        static_assert(2 * NPR * (FT / 4 + 2) <= FC, "one fix-up pass per wave");
         if (lane < 2 * NPR * nsc) {
             const int rs = lane / nsc, ci = lane - rs * nsc;
             uint64_t mm = fxm;
@@ -738,7 +777,8 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
             const int cl = __builtin_ctzll(mm); /* the column's lane in the uniform pass */
             const int o = wv + NW * rs;       /* the wave's rows: wv + NW * (2 pr + u) */
             const int r = o0r + o;
-            if (r < a.Ro) {
+            {
+                const bool ok = r < a.Ro;
                 const int ic = FT / 2 + 2 * (o0c + cl);
                 f2 v[FT];
 #pragma unroll
@@ -757,11 +797,32 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
                     : __builtin_amdgcn_make_buffer_rsrc(g.anext[item] + (int64_t)b * a.Ro * a.Co, 0, 4 * a.Ro * a.Co, 0x00020000);
                 const int pitchA = a.last ? a.PC : a.Co;
                 const int vo = 4 * (o0c + cl);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.x), rA, vo, 4 * r * pitchA, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.x), rP, vo, 4 * (r * a.PC + a.offC), 0);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.y), rP, vo, 4 * ((a.offR + r) * a.PC), 0);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.y), rP, vo, 4 * ((a.offR + r) * a.PC + a.offC), 0);
+                if (fsel) {
+                    fcls(hg.x, ok);
+                    fcls(lw.y, ok);
+                    fcls(hg.y, ok);
+                    if (a.last) fcls(lw.x, ok);
+                }
+                if (ok) {
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.x), rA, vo, 4 * r * pitchA, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.x), rP, vo, 4 * (r * a.PC + a.offC), 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.y), rP, vo, 4 * ((a.offR + r) * a.PC), 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hg.y), rP, vo, 4 * ((a.offR + r) * a.PC + a.offC), 0);
+                }
             }
+        }
+    }
+    if (fsel) { /* the wave's slot count and its counters (lane 0 took every call) */
+        uint32_t mx = f_mx;
+#pragma unroll
+        for (int o = 32; o; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        if (lane == 0) {
+            wslot[0] = f_cnt;
+            const int sh8 = blockIdx.x & (NSHARD - 1);
+            if (f_below) atomicAdd(&sst->below[sh8], (unsigned long long)f_below);
+            if (f_eq) atomicAdd(&sst->eq_lo[sh8], (unsigned long long)f_eq);
+            if (mx) atomicMax(&sst->maxkey[sh8], mx);
+            if (f_cnt > (uint32_t)FSL_KEYS) atomicOr(&sst->overflow, 1u);
         }
     }
     WTP_FPROBE(3);
@@ -1467,11 +1528,11 @@ static void fwd_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
     hipLaunchKernelGGL(k_fwd_level<FT>, dim3(grid), dim3(FB_THREADS), fwd_lds(tp.F, FT > 0), s, g, taps_of<FT>(tp));
 }
 template <int FT, bool EDGE>
-static void fwd_int_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
+static void fwd_int_go(const FwdGroup& g, int grid, const Taps& tp, const FwdSel& fs, hipStream_t s) {
     FwdIntTaps t;
     memset(&t, 0, sizeof t);
     for (int j = 0; j < FT; ++j) t.t[j] = f2{tp.f[0][j], tp.f[1][j]};
-    hipLaunchKernelGGL((k_fwd_int<FT, EDGE>), dim3(grid), dim3(FB_THREADS), fwd_int_lds(tp.F), s, g, t);
+    hipLaunchKernelGGL((k_fwd_int<FT, EDGE>), dim3(grid), dim3(FB_THREADS), fwd_int_lds(tp.F), s, g, t, fs);
 }
 
 /* The interior rectangle of a forward level's tile grid (k_fwd_int's tiles): a tile row is
@@ -1637,16 +1698,16 @@ static void fwd_general(const FwdGroup& g, int grid, const Taps& tp, hipStream_t
     }
 }
 template <bool EDGE>
-static void fwd_interior_go(const FwdGroup& g, int grid, const Taps& tp, hipStream_t s) {
+static void fwd_interior_go(const FwdGroup& g, int grid, const Taps& tp, const FwdSel& fs, hipStream_t s) {
     switch (tp.F) {
-    case 2: fwd_int_go<2, EDGE>(g, grid, tp, s); break;
-    case 4: fwd_int_go<4, EDGE>(g, grid, tp, s); break;
-    case 6: fwd_int_go<6, EDGE>(g, grid, tp, s); break;
-    case 8: fwd_int_go<8, EDGE>(g, grid, tp, s); break;
-    case 10: fwd_int_go<10, EDGE>(g, grid, tp, s); break;
-    case 12: fwd_int_go<12, EDGE>(g, grid, tp, s); break;
-    case 16: fwd_int_go<16, EDGE>(g, grid, tp, s); break;
-    case 18: fwd_int_go<18, EDGE>(g, grid, tp, s); break;
+    case 2: fwd_int_go<2, EDGE>(g, grid, tp, fs, s); break;
+    case 4: fwd_int_go<4, EDGE>(g, grid, tp, fs, s); break;
+    case 6: fwd_int_go<6, EDGE>(g, grid, tp, fs, s); break;
+    case 8: fwd_int_go<8, EDGE>(g, grid, tp, fs, s); break;
+    case 10: fwd_int_go<10, EDGE>(g, grid, tp, fs, s); break;
+    case 12: fwd_int_go<12, EDGE>(g, grid, tp, fs, s); break;
+    case 16: fwd_int_go<16, EDGE>(g, grid, tp, fs, s); break;
+    case 18: fwd_int_go<18, EDGE>(g, grid, tp, fs, s); break;
     default: break;
     }
 }
@@ -1678,7 +1739,20 @@ static void inv_interior_go(const InvGroup& g, int grid, const Taps& tp, hipStre
     }
 }
 
-void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) {
+/* fused selection: a level of (B, R, C) images runs only in k_fwd_int (the interior rectangle and
+ * the edge form, as launch_fwd_levels dispatches it with interior mode 2 or 3), whose waves classify
+ * what they write; the slots are one per wave of every tile */
+bool fwd_level_fused_ok(const FwdItem& x, const Taps& tp, int64_t* slots, bool any_mode) {
+    const FwdArgs a = fwd_args(x);
+    int r0, nr, c0, nc;
+    if ((!any_mode && g_fb_interior.load(std::memory_order_relaxed) < 2) || !fwd_int_filter(tp.F) || !fb_tiled_ok(x.B, x.R, x.C, tp) ||
+        !fwd_interior(a, tp.F, &r0, &nr, &c0, &nc))
+        return false;
+    *slots = (int64_t)a.tilesR * a.tilesC * x.B * (FB_THREADS / 64);
+    return true;
+}
+
+void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s, bool fused) {
     std::vector<FwdArgs> args(n);
     std::vector<int64_t> tiles(n);
     for (int i = 0; i < n; ++i) {
@@ -1699,6 +1773,17 @@ void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) 
             g.in[m] = args[grp[m]].in;
             g.anext[m] = args[grp[m]].anext;
             g.P[m] = args[grp[m]].P;
+        }
+        /* fused selection: the items' slots (a fused launch group holds at most SEG_PER_LAUNCH
+         * chains, so at most that many items of one level) */
+        FwdSel fs;
+        memset(&fs, 0, sizeof fs);
+        if (fused && it[grp[0]].fslot && g.n <= SEG_PER_LAUNCH) {
+            fs.on = 1;
+            for (int m = 0; m < g.n; ++m) {
+                fs.slots[m] = it[grp[m]].fslot;
+                fs.hdr[m] = it[grp[m]].fhdr;
+            }
         }
         int r0, nr, c0, nc;
         const int mode = g_fb_interior.load(std::memory_order_relaxed);
@@ -1725,11 +1810,13 @@ void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) 
                 ga.dv_per = make_fastdiv((uint32_t)ga.tiles / (uint32_t)B);
                 ga.dv_tc = make_fastdiv((uint32_t)g.geo.tilesC);
                 ga.dv_side = make_fastdiv((uint32_t)g.geo.tilesC);
-                fwd_interior_go<true>(ga, ga.n * ga.tiles, tp, s);
+                fwd_interior_go<true>(ga, ga.n * ga.tiles, tp, fs, s);
                 continue;
             }
-            fwd_interior_go<false>(gi, gi.n * gi.tiles, tp, s);
+            fwd_interior_go<false>(gi, gi.n * gi.tiles, tp, fs, s);
             if (fr == 0) continue;
+            if (fs.on) /* the frame's slots follow the interior's */
+                for (int m = 0; m < g.n; ++m) fs.slots[m] += (int64_t)gi.tiles * (FB_THREADS / 64) * FSL_WORDS;
             g.geo.frame = 1;
             g.tiles = fr * B;
             g.dv_tiles = make_fastdiv((uint32_t)g.tiles);
@@ -1737,7 +1824,7 @@ void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s) 
             g.dv_tc = make_fastdiv((uint32_t)g.geo.tilesC);
             g.dv_side = make_fastdiv((uint32_t)std::max(1, g.geo.tilesC - nc));
             if (mode >= 2) {
-                fwd_interior_go<true>(g, g.n * g.tiles, tp, s);
+                fwd_interior_go<true>(g, g.n * g.tiles, tp, fs, s);
                 continue;
             }
         }

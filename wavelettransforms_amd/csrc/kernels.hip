@@ -460,7 +460,7 @@ __device__ __forceinline__ void collect_count(const float4 (&v)[IT], bool full, 
 /* the rest of a chunk: the block's counters into the segment's (8-way sharded agent atomics), the
  * inside keys bucketed by key range (LDS histogram, the block's returning reservation atomics all
  * in flight at once) and scattered into the candidate buckets */
-template <int CT>
+template <int CT, int STGN = STG>
 __device__ __forceinline__ void collect_finish(const SegDesc& sd, SelState* __restrict__ st, uint32_t* __restrict__ cand,
                                                uint32_t kl, uint32_t sh, uint32_t below, uint32_t eql, uint32_t mx,
                                                uint32_t cnt, uint32_t* lsub, uint32_t* lbase, uint32_t* stage,
@@ -480,7 +480,7 @@ __device__ __forceinline__ void collect_finish(const SegDesc& sd, SelState* __re
     int total = 0;
     uint32_t cmax = 0;
     for (int w = 0; w < CT / 64; ++w) { total += wtot[w]; cmax = max(cmax, wred[w][3]); }
-    const bool ovf = cmax > (uint32_t)STG;
+    const bool ovf = cmax > (uint32_t)STGN;
     if (threadIdx.x == 0) {
         unsigned long long a0 = 0, a1 = 0;
         uint32_t m2 = 0;
@@ -1042,6 +1042,262 @@ __global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelHeader* __restr
         const uint32_t nsh = (gridDim.x - sh + NSHARD - 1) / NSHARD; /* blocks of this shard */
         const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);     /* shards with blocks */
         if (atomicAdd(&br->arrive[sh][0], 1u) == nsh - 1u && atomicAdd(&br->arrive[0][16], 1u) == nact - 1u)
+            head->parity = q + 1u;
+    }
+}
+
+/* ------------------------------------------------------ fused selection --- */
+/* k_fwin: the window of a fused segment before its forward (wtp_internal.h).  FWIN_NP blocks of
+ * 1024 threads per segment, each transforming one patch of FWIN_PS^2 input samples in LDS --
+ * pywt's periodization analysis at each level, the patch's own periodic extension -- and adding
+ * the keys of every coefficient of every level to the segment's histogram (the FWIN_NP patches
+ * give M_SAMPLE_WIN keys in the levels' population proportions); the segment's last block searches
+ * the window as k_window does over its sample and leaves the histogram zeroed.  The sample is an
+ * estimate: a window that misses the ranks is caught by the select, which then takes its exact
+ * full-scan path, so the patches decide speed, never the result.  Patches sit at the centres of a
+ * 4 x 4 Latin-square layout of the image (images b = patch % B).  Rows of the LDS images are
+ * FWIN_PP = 129 floats apart: the row pass's lanes walk consecutive rows, conflict-free. */
+constexpr int FWIN_RUN = 4; /* consecutive outputs per thread item: their samples shared in registers */
+constexpr int FWIN_PP = FWIN_PS + 1;
+template <int FT>
+__global__ __launch_bounds__(FWIN_THREADS) void k_fwin(FwinTable t, SelHeader* __restrict__ head) {
+    constexpr int PS = FWIN_PS, PP = FWIN_PP, NS = 2 * FWIN_RUN + FT - 2;
+    __shared__ float A[PS * PP]; /* the patch, then each level's approximation */
+    __shared__ float T[PS * PP]; /* a level's row-pass output: L | H halves of each row */
+    __shared__ WindowLds<FWIN_THREADS> wl;
+    __shared__ int s_last;
+    const int si = blockIdx.x / FWIN_NP, pt = blockIdx.x - si * FWIN_NP;
+    const FwinSeg& sg = t.s[si];
+    for (int i = threadIdx.x; i < WindowLds<FWIN_THREADS>::FBP * FWIN_THREADS; i += FWIN_THREADS) wl.h[i] = 0;
+    if (threadIdx.x < 2) wl.found[threadIdx.x] = -1;
+    auto key = [&](float v) { atomicAdd(&wl.h[key_bin(abs_key(v))], 1u); };
+    {
+        /* eighths of the free range: rows 1, 3, 5, 7 against columns 3, 7, 1, 5 */
+        const int lr = 1 + 2 * (pt & 3), lc = (0x5173 >> (4 * (pt & 3))) & 0xF;
+        const int b = pt % sg.B;
+        const int r0 = (int)((int64_t)(sg.R - PS) * lr / 8), c0 = (int)((int64_t)(sg.C - PS) * lc / 8);
+        const float* x = sg.in + ((int64_t)b * sg.R + r0) * sg.C + c0;
+        constexpr int PER = PS * PS / FWIN_THREADS; /* every load in flight before the first LDS write */
+        float v[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int i = j * FWIN_THREADS + (int)threadIdx.x;
+            v[j] = x[(int64_t)(i / PS) * sg.C + (i % PS)];
+        }
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int i = j * FWIN_THREADS + (int)threadIdx.x;
+            A[(i / PS) * PP + (i % PS)] = v[j];
+        }
+    }
+    __syncthreads();
+    int N = PS; /* a power of two at every level: the periodic index is a mask */
+    for (int k = 1; k <= sg.L; ++k) {
+        const int h = N / 2, runs = (h + FWIN_RUN - 1) / FWIN_RUN; /* runs: a power of two or 1 */
+        const int lN = __builtin_ctz(N);
+        /* rows: output j of row r is sum_q f[q] x[(2j + 1 - q) mod N]; lanes take consecutive rows */
+        for (int it = threadIdx.x; it < N * runs; it += FWIN_THREADS) {
+            const int ru = it >> lN, r = it - (ru << lN), j0 = ru * FWIN_RUN;
+            float v[NS];
+#pragma unroll
+            for (int m = 0; m < NS; ++m) v[m] = A[r * PP + ((2 * j0 + 2 - FT + m) & (N - 1))];
+#pragma unroll
+            for (int u = 0; u < FWIN_RUN; ++u) {
+                float lo = 0.0f, hi = 0.0f;
+#pragma unroll
+                for (int q = 0; q < FT; ++q) {
+                    lo += t.lo[q] * v[2 * u + FT - 1 - q];
+                    hi += t.hi[q] * v[2 * u + FT - 1 - q];
+                }
+                if (j0 + u < h) { T[r * PP + j0 + u] = lo; T[r * PP + h + j0 + u] = hi; }
+            }
+        }
+        __syncthreads();
+        /* columns: lanes take consecutive columns */
+        for (int it = threadIdx.x; it < N * runs; it += FWIN_THREADS) {
+            const int ru = it >> lN, c = it - (ru << lN), i0 = ru * FWIN_RUN;
+            float v[NS];
+#pragma unroll
+            for (int m = 0; m < NS; ++m) v[m] = T[((2 * i0 + 2 - FT + m) & (N - 1)) * PP + c];
+#pragma unroll
+            for (int u = 0; u < FWIN_RUN; ++u) {
+                float lo = 0.0f, hi = 0.0f;
+#pragma unroll
+                for (int q = 0; q < FT; ++q) {
+                    lo += t.lo[q] * v[2 * u + FT - 1 - q];
+                    hi += t.hi[q] * v[2 * u + FT - 1 - q];
+                }
+                if (i0 + u < h) {
+                    key(hi);
+                    if (c >= h) key(lo);           /* a detail band */
+                    else if (k == sg.L) key(lo);   /* the last level's approximation */
+                    if (c < h) A[(i0 + u) * PP + c] = lo; /* the next level's input */
+                }
+            }
+        }
+        __syncthreads();
+        N = h;
+    }
+    /* this patch's counts into the segment's histogram; the last patch block takes the window */
+    uint32_t* gh = t.gh + (size_t)si * FWIN_HW;
+    /* agent-scope atomics (performed at the coherence point), drained before the arrival -- no
+     * release fence, whose L2 write-back per block cost ~0.6 us a block, serialised (MI355X_MICROARCH:
+     * __threadfence); the last block reads the counts with sc1 loads */
+    for (int i = threadIdx.x; i < NB; i += FWIN_THREADS)
+        if (wl.h[i]) atomicAdd(&gh[i], wl.h[i]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&gh[NB], 1u) == (uint32_t)(FWIN_NP - 1);
+    __syncthreads();
+    if (!s_last) return; /* block-uniform */
+    for (int i = threadIdx.x; i < WindowLds<FWIN_THREADS>::FBP * FWIN_THREADS; i += FWIN_THREADS) {
+        wl.h[i] = i < NB ? ldc<true>(gh + i) : 0u;
+        if (i <= NB) gh[i] = 0; /* zero for the next launch (the counter too) */
+    }
+    if (threadIdx.x < 2) wl.found[threadIdx.x] = -1;
+    __syncthreads();
+    SegDesc sd = {};
+    sd.n = sg.n;
+    sd.r0 = sg.r0;
+    sd.above = sg.above;
+    sd.nsub_log2 = sg.nsub_log2;
+    uint32_t kl, kh, sh;
+    window_search<FWIN_THREADS, M_SAMPLE_WIN>(sd, wl, &kl, &kh, &sh);
+    if (threadIdx.x == 0) { /* the window, and the forward's counters zeroed */
+        FslHeader* hd = sg.hdr;
+        hd->kl = kl;
+        hd->kh = kh;
+        hd->shift = sh;
+        hd->overflow = 0;
+    }
+    if (threadIdx.x < NSHARD) {
+        sg.hdr->maxkey[threadIdx.x] = 0;
+        sg.hdr->below[threadIdx.x] = 0;
+        sg.hdr->eq_lo[threadIdx.x] = 0;
+    }
+}
+
+/* k_fslot_collect: a fused group's bucket pass over its wave slots (k_fwd_int's inside keys).
+ * A wave takes 64 slots, two per load: lanes 0-31 read words 0-31 of one slot and lanes 32-63 of
+ * the next -- one 128-byte line per slot, which holds the count and up to 31 keys (a wave of the
+ * forward classifies 768 coefficients, ~18 of them inside the window); a slot with more keys has
+ * its second line read too.  Lane word j >= 1 holds key j - 1 and is kept when j <= the count.  The
+ * keys are then bucketed as collect_finish buckets a chunk's (a block LDS histogram over the
+ * window's buckets, one reservation per non-empty bucket, the scatter).  The forward already
+ * counted the keys below and at kl and the largest key.  Housekeeping as k_collect: the idle region
+ * cleared, the zero counts reset, the last block flips the parity. */
+constexpr int FSC_SPW = FSC_SLOTS / (FSC_THREADS / 64); /* slots per wave */
+constexpr int FSC_NP = FSC_SPW / 2;                     /* slot pairs per wave */
+__global__ __launch_bounds__(FSC_THREADS) void k_fslot_collect(SegTable t, SelHeader* __restrict__ head,
+                                                               uint32_t* __restrict__ cand, wtp_result* __restrict__ res) {
+    static_assert(FSL_WORDS == 64 && FSC_NP <= 32, "two 32-word halves per slot, a pair bit per mask bit");
+    __shared__ uint32_t lsub[NSUB_MAX];
+    __shared__ uint32_t lbase[NSUB_MAX];
+    __shared__ uint32_t s_any;
+    const uint32_t q = head->parity;
+    {   /* clear this block's slice of the idle region */
+        uint4* idle = reinterpret_cast<uint4*>(sel_region(head, q ^ 1u));
+        constexpr int NV4 = (int)(SEL_REGION / 16);
+        const int per = (NV4 + (int)gridDim.x - 1) / (int)gridDim.x;
+        for (int i = threadIdx.x; i < per; i += FSC_THREADS) {
+            const int j = (int)blockIdx.x * per + i;
+            if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    const int si = find_seg(t, blockIdx.x);
+    const SegDesc& sd = t.s[si];
+    SelState* st = sel_region(head, q) + sd.slot;
+    const FslHeader* hd = reinterpret_cast<const FslHeader*>(sd.fsl);
+    if ((int)blockIdx.x == sd.blk_begin) { /* the segment's first block: the head into the SelState */
+        if (threadIdx.x == 0) {
+            res[sd.res].zero_count = 0; /* the inverse adds */
+            st->kl = hd->kl;
+            st->kh = hd->kh;
+            st->shift = hd->shift;
+            st->overflow = hd->overflow;
+        }
+        if (threadIdx.x < NSHARD) {
+            st->below[threadIdx.x] = hd->below[threadIdx.x];
+            st->eq_lo[threadIdx.x] = hd->eq_lo[threadIdx.x];
+            st->maxkey[threadIdx.x] = hd->maxkey[threadIdx.x];
+        }
+    }
+    const int nsub = 1 << sd.nsub_log2;
+    for (int i = threadIdx.x; i < nsub; i += FSC_THREADS) lsub[i] = 0;
+    if (threadIdx.x == 0) s_any = 0;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, hl = lane >> 5, wj = lane & 31;
+    const int s0 = ((int)blockIdx.x - sd.blk_begin) * FSC_SLOTS + wv * FSC_SPW;
+    const int ns = max(0, min(FSC_SPW, sd.fsl_n - s0)); /* this wave's slots (uniform) */
+    const uint32_t* base = sd.fsl + FSL_HDR_WORDS + (int64_t)s0 * FSL_WORDS;
+    uint32_t w[FSC_NP];
+#pragma unroll
+    for (int p = 0; p < FSC_NP; ++p) w[p] = 2 * p + hl < ns ? base[(int64_t)(2 * p + hl) * FSL_WORDS + wj] : 0u;
+    const uint32_t kl = hd->kl, sh = hd->shift;
+    uint32_t keep = 0, ext = 0; /* bit p: this lane's first-line word of pair p is a key; pair p has a second line */
+#pragma unroll
+    for (int p = 0; p < FSC_NP; ++p) {
+        const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)w[p], 0), c1 = (uint32_t)__builtin_amdgcn_readlane((int)w[p], 32);
+        const uint32_t c = min(hl ? c1 : c0, (uint32_t)FSL_KEYS);
+        if (2 * p + hl < ns && wj >= 1 && (uint32_t)wj <= c) keep |= 1u << p;
+        if (max(c0, c1) > 31u) ext |= 1u << p; /* uniform */
+    }
+    /* a second-line word: key 31 + wj of its slot, kept when 32 + wj <= the count */
+    auto second = [&](int p, uint32_t* kv) {
+        const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)w[p], 0), c1 = (uint32_t)__builtin_amdgcn_readlane((int)w[p], 32);
+        const uint32_t c = min(hl ? c1 : c0, (uint32_t)FSL_KEYS);
+        const bool ok = 2 * p + hl < ns && (uint32_t)(32 + wj) <= c;
+        *kv = ok ? base[(int64_t)(2 * p + hl) * FSL_WORDS + 32 + wj] : 0u;
+        return ok;
+    };
+    __syncthreads(); /* lsub cleared */
+    if (keep || ext) {
+#pragma unroll
+        for (int p = 0; p < FSC_NP; ++p)
+            if ((keep >> p) & 1u) atomicAdd(&lsub[(w[p] - kl - 1) >> sh], 1u);
+        for (uint32_t m = ext; m; m &= m - 1) { /* rare: a slot with more than 31 keys */
+            uint32_t kv;
+            if (second(__builtin_ctz(m), &kv)) atomicAdd(&lsub[(kv - kl - 1) >> sh], 1u);
+        }
+        if (keep) s_any = 1;
+    }
+    __syncthreads();
+    if (!s_any && !__syncthreads_or(ext != 0)) goto done; /* uniform: no key in this block */
+    {   /* one contiguous run per non-empty bucket (one returning atomic per bucket, all in flight) */
+        constexpr int PER = NSUB_MAX / FSC_THREADS;
+        uint32_t cj[PER], rj[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) cj[j] = (j * FSC_THREADS + (int)threadIdx.x < nsub) ? lsub[j * FSC_THREADS + threadIdx.x] : 0u;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) rj[j] = cj[j] ? atomicAdd(&st->sub[j * FSC_THREADS + threadIdx.x], cj[j]) : 0u;
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+            if (j * FSC_THREADS + (int)threadIdx.x < nsub) { lbase[j * FSC_THREADS + threadIdx.x] = rj[j]; lsub[j * FSC_THREADS + threadIdx.x] = 0; }
+    }
+    __syncthreads();
+    {
+        const int64_t bcap = sd.bucket_cap;
+        uint32_t* out = cand + sd.cand_off;
+        auto put = [&](uint32_t k) {
+            const uint32_t b = (k - kl - 1) >> sh;
+            const uint32_t at = lbase[b] + atomicAdd(&lsub[b], 1u);
+            if (at < bcap) out[(int64_t)b * bcap + at] = k; /* counted beyond capacity: the select sees it */
+        };
+#pragma unroll
+        for (int p = 0; p < FSC_NP; ++p)
+            if ((keep >> p) & 1u) put(w[p]);
+        for (uint32_t m = ext; m; m &= m - 1) {
+            uint32_t kv;
+            if (second(__builtin_ctz(m), &kv)) put(kv);
+        }
+    }
+done:
+    __syncthreads(); /* every wave has read the parity */
+    if (threadIdx.x == 0) {
+        BarState* br = bar_region(head, q);
+        const uint32_t shd = blockIdx.x & (NSHARD - 1);
+        const uint32_t nsh = (gridDim.x - shd + NSHARD - 1) / NSHARD;
+        const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);
+        if (atomicAdd(&br->arrive[shd][0], 1u) == nsh - 1u && atomicAdd(&br->arrive[0][16], 1u) == nact - 1u)
             head->parity = q + 1u;
     }
 }
@@ -2372,6 +2628,23 @@ void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_resu
     else
         hipLaunchKernelGGL((k_collect_t<COLLECT_THREADS, COLLECT_IT, false>), dim3(collect_blocks(t)),
                            dim3(COLLECT_THREADS), 0, s, t, head, cand, res);
+}
+void launch_fwin(const FwinTable& t, SelHeader* head, hipStream_t s) {
+    const dim3 g(t.nseg * FWIN_NP), b(FWIN_THREADS);
+    switch (t.F) {
+    case 2: hipLaunchKernelGGL(k_fwin<2>, g, b, 0, s, t, head); break;
+    case 4: hipLaunchKernelGGL(k_fwin<4>, g, b, 0, s, t, head); break;
+    case 6: hipLaunchKernelGGL(k_fwin<6>, g, b, 0, s, t, head); break;
+    case 8: hipLaunchKernelGGL(k_fwin<8>, g, b, 0, s, t, head); break;
+    case 10: hipLaunchKernelGGL(k_fwin<10>, g, b, 0, s, t, head); break;
+    case 12: hipLaunchKernelGGL(k_fwin<12>, g, b, 0, s, t, head); break;
+    case 16: hipLaunchKernelGGL(k_fwin<16>, g, b, 0, s, t, head); break;
+    case 18: hipLaunchKernelGGL(k_fwin<18>, g, b, 0, s, t, head); break;
+    default: break; /* the host fuses only k_fwd_int's filters */
+    }
+}
+void launch_fslot_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s) {
+    hipLaunchKernelGGL(k_fslot_collect, dim3(t.nblk), dim3(FSC_THREADS), 0, s, t, head, cand, res);
 }
 void launch_minprune(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
                      void* mp, uint32_t* tiecnt, hipStream_t s) {

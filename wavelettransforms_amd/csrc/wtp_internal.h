@@ -93,6 +93,9 @@ struct SegDesc {
     int32_t nsub_log2; /* 6..10                                                          */
     int32_t bucket_cap;
     uint64_t res_step_fx; /* k_resident: (n - SAMPLE_GROUP) / (RES_MS / SAMPLE_GROUP - 1) in 32.32 fixed point */
+    const uint32_t* fsl;  /* fused selection: the segment's slot area (FslHeader, then the wave slots) */
+    int32_t fsl_n;        /* ... and its number of wave slots                              */
+    int32_t pad_f;
 };
 
 struct SegTable {
@@ -108,6 +111,7 @@ struct SegTable {
     SegDesc s[SEG_PER_LAUNCH];
 };
 static_assert(sizeof(SegTable) <= 4096, "k_resident's kernel argument");
+
 
 /* per-slot selection state.  Slots are the positions of a segment inside its launch group
  * (0..SEG_PER_LAUNCH-1); the SelState slots sit at the very start of every workspace
@@ -163,6 +167,66 @@ __host__ __device__ inline BarState* bar_region(void* head, uint32_t q) {
 }
 
 enum SelMode : int32_t { MODE_CAND = 1, MODE_WINDOW = 2, MODE_FULL = 3, MODE_FAULT = 99 };
+
+/* ---- fused selection (large DWT segments, every forward level in k_fwd_int) ----
+ * k_fwin derives each segment's window BEFORE its forward, from the periodized transform of
+ * FWIN_NP patches of FWIN_PS^2 input samples (= M_SAMPLE_WIN coefficients in the population's
+ * level proportions); every k_fwd_int wave then classifies the coefficients it writes to P against
+ * it (counts below / equal to kl into the segment's SelState, the keys inside (kl, kh] into a slot
+ * of its own: FSL_WORDS words, the count then up to FSL_KEYS keys; more sets the overflow flag and
+ * sends the segment to the exact full-scan select), and k_fslot_collect buckets the slots' keys
+ * as k_collect buckets a chunk's -- so P is never re-read for the selection. */
+constexpr int FSL_WORDS = 64;
+constexpr int FSL_KEYS = FSL_WORDS - 1;
+constexpr int FWIN_PS = 128;
+constexpr int FWIN_NP = 4;
+constexpr int FWIN_THREADS = 1024;
+constexpr int FSC_THREADS = 256; /* k_fslot_collect: 64 wave slots per wave, a slot word per lane */
+constexpr int FSC_SLOTS = 64 * (FSC_THREADS / 64);
+constexpr int FWIN_F_MAX = 18;   /* k_fwd_int's longest filter */
+static_assert(FWIN_NP * FWIN_PS * FWIN_PS == M_SAMPLE_WIN, "k_fwin's sample is k_window's");
+/* The head of a fused tensor's slot area: its window (k_fwin) and the forward's counters -- the
+ * forward never touches the SelState regions, so a group's bucket pass and select can run on the
+ * side stream while the next group's forward runs (the areas are double-buffered by group parity);
+ * k_fslot_collect copies it into its SelState slot. */
+struct alignas(256) FslHeader {
+    /* the window on a line of its own: every forward workgroup reads it, and a line that also
+     * took the counters' atomics would be re-fetched by each (measured: the level-1 forward
+     * 785 -> 1361 us with window and counters on shared lines) */
+    uint32_t kl, kh, shift;
+    uint32_t pad0[29];
+    unsigned long long below[NSHARD]; /* as SelState: below and eq_lo on one line, max on the next */
+    unsigned long long eq_lo[NSHARD];
+    uint32_t maxkey[NSHARD];
+    uint32_t overflow;
+    uint32_t pad1[23];
+};
+static_assert(sizeof(FslHeader) == 512, "FslHeader lines");
+constexpr int FSL_HDR_WORDS = (int)(sizeof(FslHeader) / 4);
+struct FwdSel { /* k_fwd_int's fused-selection argument (on = 0: off) */
+    int32_t on, pad;
+    FslHeader* hdr[SEG_PER_LAUNCH];    /* per item of the launch: its tensor's slot-area head */
+    uint32_t* slots[SEG_PER_LAUNCH];   /* per item: its wave slots for this launch's tiles */
+};
+struct FwinSeg {
+    const float* in; /* the segment's input images (B x R x C) */
+    FslHeader* hdr;  /* the window goes here (its counters are zeroed) */
+    int64_t n, r0;
+    int32_t above, nsub_log2, B, R, C, L;
+};
+struct FwinTable {
+    int32_t nseg, F;
+    float lo[FWIN_F_MAX], hi[FWIN_F_MAX];
+    uint32_t* gh; /* the persistent histograms (fwin_hist): zero between launches */
+    FwinSeg s[SEG_PER_LAUNCH];
+};
+/* k_fwin's per-segment histogram (NB bins) and arrival counter in the workspace's persistent
+ * region (zeroed by wtp_workspace_init; the segment's last patch block re-zeroes what it read) */
+constexpr int FWIN_HW = (NB + 1 + 31) / 32 * 32;
+constexpr size_t FWIN_HIST_BYTES = (size_t)SEG_PER_LAUNCH * FWIN_HW * 4;
+__host__ __device__ inline uint32_t* fwin_hist(void* head) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(head) + sizeof(SelHeader) + 2 * SEL_REGION);
+}
 
 /* filter taps as a kernel argument (scalar-loaded, uniform across the wave) */
 struct Taps {
@@ -305,7 +369,14 @@ struct FwdItem { /* one image batch's analysis level k: (B, R, C) in -> P detail
     float* P;
     int64_t PR, PC, offR, offC;
     int last;
+    uint32_t* fslot = nullptr; /* fused selection: the item's wave slots for this level (null: off) */
+    FslHeader* fhdr = nullptr; /* ... and its tensor's slot-area head */
 };
+/* fused selection: the wave slots one forward level of (B, R, C) images fills (k_fwd_int's tiles
+ * x waves); false when some launch of that level would not be k_fwd_int (no classification) */
+bool fwd_level_fused_ok(const FwdItem& x, const Taps& tp, int64_t* slots, bool any_mode = false);
+void launch_fwin(const FwinTable& t, SelHeader* head, hipStream_t s);
+void launch_fslot_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s);
 struct InvItem { /* one image batch's synthesis level k -> y (B, outH, outW) */
     const float* a_src; /* nullptr: the packed cA */
     int64_t a_bs, lda;
@@ -317,7 +388,7 @@ struct InvItem { /* one image batch's synthesis level k -> y (B, outH, outW) */
     int64_t outH, outW;
     unsigned long long* zc;
 };
-void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s);
+void launch_fwd_levels(const FwdItem* it, int n, const Taps& tp, hipStream_t s, bool fused = false);
 void launch_inv_levels(const InvItem* it, int n, const Taps& tp, hipStream_t s);
 int fb_set_interior(int mode); /* filter-bank kernel choice 0..2 (wtp_set_interior); returns the previous */
 void launch_fwd_level(const float* in, int64_t B, int64_t R, int64_t C, const Taps& tp, float* anext, float* P,

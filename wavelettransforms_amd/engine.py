@@ -230,11 +230,19 @@ def set_resident(enabled):
 
 def set_pipeline(enabled):
     """Overlap each launch group's selection with the next group's forward transform on a side
-    stream (True / 1, the default), or run every group on a lane stream of its own, staggered, with
-    the selections on the side stream (2); False / 0 one stream (include/wtprune.h
-    wtp_set_pipeline).  Returns the previous mode."""
+    stream (True / 1, the default); False / 0 one stream (include/wtprune.h wtp_set_pipeline).
+    Returns the previous mode."""
     mode = (1 if enabled else 0) if isinstance(enabled, bool) else int(enabled)
     return int(N.lib().wtp_set_pipeline(mode))
+
+
+def set_fused_select(enabled):
+    """Fused selection for launch groups of large wavelet-transformed tensors (True / 1, the
+    default): the window from a transform of input patches before the forward, the forward
+    classifying the coefficients it writes, no re-read of the packed array; False / 0 the
+    window / collect / select passes over the packed array (include/wtprune.h
+    wtp_set_fused_select).  Identical results either way.  Returns the previous mode."""
+    return int(N.lib().wtp_set_fused_select(1 if enabled else 0))
 
 
 def set_interior(enabled):
