@@ -63,6 +63,8 @@ typedef struct wtp_result {
     int32_t eff_level;      /* min(level, calculate_max_level(shape))     :64-65     */
     int32_t path;           /* selection: 1 window candidates, 2 window edges, 3 full scan,
                                4 the one-launch small path (exact three-digit radix select);
+                               + 8 (9, 10, 11): the fused selection's patch window missed the ranks
+                               and the segment was selected again over its coefficients;
                                99 = the resident launch's grid was not co-resident (results invalid) */
 } wtp_result;
 

@@ -19,7 +19,7 @@ from tests import golden_io as G
 
 pytestmark = pytest.mark.gpu
 
-MODE_CAND, MODE_FULL = 1, 3
+MODE_CAND, MODE_FULL, RETRIED = 1, 3, 8
 # each >= 2^22 packed coefficients, tight (dims divisible by 2^L), images >= 128 x 128, and at
 # level <= 4 every forward level of these images has interior tiles (k_fwd_int throughout)
 SHAPES = [(2048, 2048), (2, 1024, 2048), (1, 2048, 3072)]
@@ -93,11 +93,11 @@ def _patch_origins(R, C):
 
 
 @pytest.mark.timeout(300)
-def test_window_miss_takes_the_exact_full_scan(eng):
+def test_window_miss_is_selected_again_over_p(eng):
     """Everything outside the four patches scaled by 16: the patches' window sits far below the
-    tensor's percentile, the select sees the ranks above it and scans the packed array in full;
-    the unfused form (its window sampled from the packed array itself) holds the ranks.  Same
-    results either way, and equal to the oracle."""
+    tensor's percentile, the select sees the ranks above it and the retry launches select the
+    segment again from a window sampled over its packed array (path + 8), as the unfused form
+    does from the start.  Same results either way, and equal to the oracle."""
     R, C = 2048, 2048
     x = eng.synth((R, C), 5, 0, _e((R, C), 0))
     scale = torch.full((R, C), 16.0, device=x.device)
@@ -107,7 +107,7 @@ def test_window_miss_takes_the_exact_full_scan(eng):
     a = _run(eng, [x], True, "db8", 4, 50.0)
     b = _run(eng, [x], False, "db8", 4, 50.0)
     _same(a, b)
-    assert a[1][0]["path"] == MODE_FULL and b[1][0]["path"] == MODE_CAND, (a[1][0]["path"], b[1][0]["path"])
+    assert a[1][0]["path"] == RETRIED + MODE_CAND and b[1][0]["path"] == MODE_CAND, (a[1][0]["path"], b[1][0]["path"])
     ref, rr = O.prune_tensor(x.cpu().numpy(), "db8", 4, 50.0)
     assert np.array_equal(a[0][0].view(np.uint32), ref.view(np.uint32))
     assert G.f64_bits_equal(a[1][0]["thr64"], rr["thr64"])
@@ -116,8 +116,8 @@ def test_window_miss_takes_the_exact_full_scan(eng):
 @pytest.mark.timeout(300)
 def test_heavy_ties(eng):
     """Integer-valued input in {-2..2}: the haar coefficients take a handful of values, so the
-    window's bins hold many equal keys (slot overflow and bucket overflow send the select to its
-    full scan); the results still equal the unfused form and the oracle."""
+    window's bins hold many equal keys (slot overflow sends the segment to the retry, bucket
+    overflow to the full scan); the results still equal the unfused form and the oracle."""
     g = torch.Generator(device="cpu").manual_seed(3)
     xn = torch.randint(-2, 3, (2048, 2048), generator=g).float()
     x = xn.cuda()

@@ -862,6 +862,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             if (fz) { /* k_fslot_collect: one block per FSC_SLOTS wave slots */
                 sd.fsl = reinterpret_cast<const uint32_t*>(wsb(ws, p.f_off));
                 sd.fsl_n = (int32_t)p.f_slots;
+                sd.flags |= SEG_FUSED;
                 blk += (int)((p.f_slots + FSC_SLOTS - 1) / FSC_SLOTS);
             } else {
                 blk += (int)((p.pop + chunk - 1) / chunk);
@@ -916,6 +917,21 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             launch_fslot_collect(tab, head, cand, results, ss);
             if (first) stage(3, ss);
             launch_mask_select(tab, head, cand, results, thr_t, ss);
+            /* a segment whose patch window missed the ranks: the unfused window / collect / select
+             * over P, for it alone (the same table in k_collect's chunk units) */
+            SegTable rt = tab;
+            rt.retry = 1;
+            int rb = 0;
+            for (int i = 0; i < rt.nseg; ++i) {
+                SegDesc& sd = rt.s[i];
+                sd.flags &= ~SEG_FUSED;
+                sd.fsl = nullptr;
+                sd.fsl_n = 0;
+                sd.blk_begin = rt.blk_begin[i] = rb;
+                rb += (int)((sd.n + CHUNK - 1) / CHUNK);
+            }
+            rt.nblk = rb;
+            launch_fused_retry(rt, head, cand, results, thr_t, ss);
         } else if (resident) {
             if (first) stage(1, ss);
             if (first) { stage(2, ss); stage(3, ss); }

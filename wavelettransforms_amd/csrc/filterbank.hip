@@ -812,17 +812,26 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
             }
         }
     }
-    if (fsel) { /* the wave's slot count and its counters (lane 0 took every call) */
+    if (fsel) { /* the wave's slot count (lane 0 took every call); the workgroup's counters */
+        __shared__ uint32_t s_fc[FB_THREADS / 64][3];
         uint32_t mx = f_mx;
 #pragma unroll
         for (int o = 32; o; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
         if (lane == 0) {
             wslot[0] = f_cnt;
-            const int sh8 = blockIdx.x & (NSHARD - 1);
-            if (f_below) atomicAdd(&sst->below[sh8], (unsigned long long)f_below);
-            if (f_eq) atomicAdd(&sst->eq_lo[sh8], (unsigned long long)f_eq);
-            if (mx) atomicMax(&sst->maxkey[sh8], mx);
+            s_fc[wv][0] = f_below;
+            s_fc[wv][1] = f_eq;
+            s_fc[wv][2] = mx;
             if (f_cnt > (uint32_t)FSL_KEYS) atomicOr(&sst->overflow, 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t b = 0, e = 0, m = 0;
+#pragma unroll
+            for (int w = 0; w < FB_THREADS / 64; ++w) { b += s_fc[w][0]; e += s_fc[w][1]; m = max(m, s_fc[w][2]); }
+            const int sh8 = blockIdx.x & (NSHARD - 1);
+            if (b | e) atomicAdd(&sst->be[sh8], ((unsigned long long)e << 32) | b);
+            if (m) atomicMax(&sst->maxkey[sh8], m);
         }
     }
     WTP_FPROBE(3);

@@ -889,6 +889,13 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
         ka = (ca == 1) ? kl : kh;
         kb = (cb == 1) ? kl : kh;
     }
+    if (full && (sd.flags & SEG_FUSED)) {
+        /* a fused segment: its window came from input patches; the retry launches take it again
+         * from P (k_window / k_collect) -- nothing is published here */
+        if (publish && threadIdx.x == 0) res[sd.res].path = MODE_RETRY;
+        __syncthreads();
+        return __uint_as_float(0x7FC00000u);
+    }
     if (full) {
         /* the window missed (or a block/bucket overflowed): exact radix select over the segment */
         select_in_range<THREADS>([&](int64_t i) { return abs_key(x[i]); }, [](uint32_t) { return true; }, sd.n, 0u,
@@ -943,7 +950,7 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
         r.max_abs_bits = mk;
         r.eff_level = sd.eff_level;
         if constexpr (COH) atomicMax(&r.path, path); /* a timed-out workgroup may raise it to MODE_FAULT */
-        else r.path = path;
+        else r.path = r.path == MODE_RETRY ? path + MODE_RETRIED : path; /* the fused retry's select */
     }
     WTP_PROBE(6);
     return minp ? __uint_as_float(ka) : thr32;
@@ -952,9 +959,11 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
 /* k_window: one 1024-thread block per segment derives the window of the region k_collect is
  * about to fill (used when the window is not computed inline by every k_collect block) */
 constexpr int WIN_THREADS = 1024;
-__global__ __launch_bounds__(WIN_THREADS) void k_window(SegTable t, SelHeader* __restrict__ head) {
+__global__ __launch_bounds__(WIN_THREADS) void k_window(SegTable t, SelHeader* __restrict__ head,
+                                                         const wtp_result* __restrict__ res) {
     __shared__ WindowLds<WIN_THREADS> wl;
     const SegDesc& sd = t.s[blockIdx.x];
+    if (t.retry && res[sd.res].path != MODE_RETRY) return; /* block-uniform */
     /* the sample in passes of 16 keys a thread (groups of SAMPLE_GROUP contiguous keys spread
      * evenly over the segment, as sample_keys), histogrammed as they arrive */
     constexpr int PASS = 16 * WIN_THREADS, NPASS = M_SAMPLE_WIN / PASS;
@@ -1041,6 +1050,56 @@ __global__ __launch_bounds__(CT) void k_collect_t(SegTable t, SelHeader* __restr
         const uint32_t sh = blockIdx.x & (NSHARD - 1);
         const uint32_t nsh = (gridDim.x - sh + NSHARD - 1) / NSHARD; /* blocks of this shard */
         const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);     /* shards with blocks */
+        if (atomicAdd(&br->arrive[sh][0], 1u) == nsh - 1u && atomicAdd(&br->arrive[0][16], 1u) == nact - 1u)
+            head->parity = q + 1u;
+    }
+}
+
+/* The fused selection's retry collect: k_collect_t over the chunks of the segments whose select
+ * read MODE_RETRY only, as a grid-stride loop (a fixed small grid: when nothing missed, every block
+ * reads the records and leaves); the housekeeping as k_collect_t (idle region, parity flip). */
+template <int CT, int IT>
+__global__ __launch_bounds__(CT) void k_collect_retry(SegTable t, SelHeader* __restrict__ head, uint32_t* __restrict__ cand,
+                                                      wtp_result* __restrict__ res) {
+    constexpr int SUB = IT * CT * 4, SPLIT = CHUNK / SUB;
+    __shared__ uint32_t lsub[NSUB_MAX];
+    __shared__ uint32_t lbase[NSUB_MAX];
+    __shared__ uint32_t stage[STG * CT];
+    __shared__ uint32_t wred[CT / 64][4];
+    __shared__ int wtot[CT / 64];
+    const uint32_t q = head->parity;
+    {   /* clear this block's slice of the idle region */
+        uint4* idle = reinterpret_cast<uint4*>(sel_region(head, q ^ 1u));
+        constexpr int NV4 = (int)(SEL_REGION / 16);
+        const int per = (NV4 + (int)gridDim.x - 1) / (int)gridDim.x;
+        for (int i = threadIdx.x; i < per; i += CT) {
+            const int j = (int)blockIdx.x * per + i;
+            if (j < NV4) idle[j] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    const int total = t.nblk * SPLIT;
+    for (int bb = blockIdx.x; bb < total; bb += gridDim.x) {
+        const int tb = bb / SPLIT;
+        const int si = find_seg(t, tb);
+        const SegDesc& sd = t.s[si];
+        if (res[sd.res].path != MODE_RETRY) continue; /* block-uniform */
+        const int64_t base = (int64_t)(tb - sd.blk_begin) * CHUNK + (int64_t)(bb % SPLIT) * SUB;
+        const int len = (int)max((int64_t)0, min((int64_t)SUB, sd.n - base));
+        SelState* st = sel_region(head, q) + sd.slot;
+        if (len > 0) {
+            if ((sd.flags & SEG_ALIGNED) && len == SUB)
+                collect_body<CT, IT, true, false>(sd, st, cand, base, len, false, lsub, lbase, stage, nullptr, wred, wtot);
+            else
+                collect_body<CT, IT, false, false>(sd, st, cand, base, len, false, lsub, lbase, stage, nullptr, wred, wtot);
+        }
+        __syncthreads(); /* LDS reused by the next chunk */
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        BarState* br = bar_region(head, q);
+        const uint32_t sh = blockIdx.x & (NSHARD - 1);
+        const uint32_t nsh = (gridDim.x - sh + NSHARD - 1) / NSHARD;
+        const uint32_t nact = min((uint32_t)NSHARD, gridDim.x);
         if (atomicAdd(&br->arrive[sh][0], 1u) == nsh - 1u && atomicAdd(&br->arrive[0][16], 1u) == nact - 1u)
             head->parity = q + 1u;
     }
@@ -1172,8 +1231,7 @@ __global__ __launch_bounds__(FWIN_THREADS) void k_fwin(FwinTable t, SelHeader* _
     }
     if (threadIdx.x < NSHARD) {
         sg.hdr->maxkey[threadIdx.x] = 0;
-        sg.hdr->below[threadIdx.x] = 0;
-        sg.hdr->eq_lo[threadIdx.x] = 0;
+        sg.hdr->be[threadIdx.x] = 0;
     }
 }
 
@@ -1214,11 +1272,12 @@ __global__ __launch_bounds__(FSC_THREADS) void k_fslot_collect(SegTable t, SelHe
             st->kl = hd->kl;
             st->kh = hd->kh;
             st->shift = hd->shift;
-            st->overflow = hd->overflow;
+            if (hd->overflow) atomicOr(&st->overflow, 1u); /* other blocks may flag it too */
         }
         if (threadIdx.x < NSHARD) {
-            st->below[threadIdx.x] = hd->below[threadIdx.x];
-            st->eq_lo[threadIdx.x] = hd->eq_lo[threadIdx.x];
+            const unsigned long long be = hd->be[threadIdx.x];
+            st->below[threadIdx.x] = be & 0xFFFFFFFFull;
+            st->eq_lo[threadIdx.x] = be >> 32;
             st->maxkey[threadIdx.x] = hd->maxkey[threadIdx.x];
         }
     }
@@ -1249,16 +1308,27 @@ __global__ __launch_bounds__(FSC_THREADS) void k_fslot_collect(SegTable t, SelHe
         *kv = ok ? base[(int64_t)(2 * p + hl) * FSL_WORDS + 32 + wj] : 0u;
         return ok;
     };
+    /* a key's bucket; a key outside the window's buckets (never written by the forward, which
+     * stores only inside keys) would mean a stale slot: dropped, and the segment retried */
+    bool bad = false;
+    auto bucket = [&](uint32_t k, uint32_t* b) {
+        *b = (k - kl - 1) >> sh;
+        const bool ok = *b < (uint32_t)nsub;
+        bad = bad || !ok;
+        return ok;
+    };
     __syncthreads(); /* lsub cleared */
     if (keep || ext) {
+        uint32_t b;
 #pragma unroll
         for (int p = 0; p < FSC_NP; ++p)
-            if ((keep >> p) & 1u) atomicAdd(&lsub[(w[p] - kl - 1) >> sh], 1u);
+            if (((keep >> p) & 1u) && bucket(w[p], &b)) atomicAdd(&lsub[b], 1u);
         for (uint32_t m = ext; m; m &= m - 1) { /* rare: a slot with more than 31 keys */
             uint32_t kv;
-            if (second(__builtin_ctz(m), &kv)) atomicAdd(&lsub[(kv - kl - 1) >> sh], 1u);
+            if (second(__builtin_ctz(m), &kv) && bucket(kv, &b)) atomicAdd(&lsub[b], 1u);
         }
         if (keep) s_any = 1;
+        if (bad) atomicOr(&st->overflow, 1u);
     }
     __syncthreads();
     if (!s_any && !__syncthreads_or(ext != 0)) goto done; /* uniform: no key in this block */
@@ -1279,6 +1349,7 @@ __global__ __launch_bounds__(FSC_THREADS) void k_fslot_collect(SegTable t, SelHe
         uint32_t* out = cand + sd.cand_off;
         auto put = [&](uint32_t k) {
             const uint32_t b = (k - kl - 1) >> sh;
+            if (b >= (uint32_t)nsub) return;
             const uint32_t at = lbase[b] + atomicAdd(&lsub[b], 1u);
             if (at < bcap) out[(int64_t)b * bcap + at] = k; /* counted beyond capacity: the select sees it */
         };
@@ -1358,6 +1429,7 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_mask_select(SegTable t, cons
     const int64_t base = (int64_t)(blockIdx.x - sd.blk_begin) * CHUNK;
     const bool masked = (sd.flags & SEG_MASK) != 0;
     if (!masked && base != 0) return; /* block-uniform */
+    if (t.retry && res[sd.res].path != MODE_RETRY) return;
     const int len = (int)min((int64_t)CHUNK, sd.n - base);
     const bool full = (sd.flags & SEG_ALIGNED) && len == CHUNK;
     /* the select first: loads return in issue order (vmcnt), so chunk loads issued ahead of
@@ -2618,8 +2690,16 @@ static inline unsigned grid_for(int64_t total) {
 
 static int collect_blocks(const SegTable& t) { return t.nblk * (CHUNK / (COLLECT_IT * COLLECT_THREADS * 4)); }
 static bool window_inline(const SegTable& t) { return collect_blocks(t) <= WINDOW_INLINE_MAX_BLOCKS; }
-void launch_window(const SegTable& t, SelHeader* head, hipStream_t s) {
-    if (!window_inline(t)) hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, s, t, head);
+void launch_window(const SegTable& t, SelHeader* head, hipStream_t s, const wtp_result* res) {
+    if (!window_inline(t)) hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, s, t, head, res);
+}
+void launch_fused_retry(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(k_window, dim3(t.nseg), dim3(WIN_THREADS), 0, s, t, head, (const wtp_result*)res);
+    const int total = collect_blocks(t);
+    hipLaunchKernelGGL((k_collect_retry<COLLECT_THREADS, COLLECT_IT>), dim3(total < 512 ? total : 512), dim3(COLLECT_THREADS), 0,
+                       s, t, head, cand, res);
+    launch_mask_select(t, head, cand, res, thr_out, s);
 }
 void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s) {
     if (window_inline(t))

@@ -73,6 +73,7 @@ enum SegFlags : int32_t {
     SEG_MINPRUNE = 4,  /* min-weight pruning: rank k-1 = r0 select, k_minmask writes */
     SEG_KZERO = 8,     /* min-weight pruning with k = 0: nothing pruned              */
     SEG_LATE = 16,     /* k_resident: the late group (window first, then the chunk's loads) */
+    SEG_FUSED = 32,    /* fused selection: a window miss is retried (MODE_RETRY), not full-scanned */
 };
 
 struct SegDesc {
@@ -102,7 +103,7 @@ struct SegTable {
     int32_t nseg;
     int32_t nblk;
     int32_t nsel;      /* k_resident: selector workgroups after the nblk chunks (0: every segment selects for itself) */
-    int32_t pad;
+    int32_t retry;     /* fused selection's retry launches: only segments whose record reads MODE_RETRY */
     uint32_t res_timeout; /* k_resident: bound of every wait, in ticks of the 100 MHz wall clock */
     int32_t pad2;
     unsigned long long* stamps; /* k_resident: [0] min start, [1] max end (100 MHz ticks); null = off */
@@ -166,7 +167,10 @@ __host__ __device__ inline BarState* bar_region(void* head, uint32_t q) {
     return reinterpret_cast<BarState*>(reinterpret_cast<char*>(sel_region(head, q)) + SEG_PER_LAUNCH * sizeof(SelState));
 }
 
-enum SelMode : int32_t { MODE_CAND = 1, MODE_WINDOW = 2, MODE_FULL = 3, MODE_FAULT = 99 };
+/* MODE_RETRY: a fused segment's window missed (or its slots overflowed); the retry launches
+ * (window / collect / select over P) run it again and overwrite the record */
+enum SelMode : int32_t { MODE_CAND = 1, MODE_WINDOW = 2, MODE_FULL = 3, MODE_RETRY = 5, MODE_RETRIED = 8,
+                         MODE_FAULT = 99 };
 
 /* ---- fused selection (large DWT segments, every forward level in k_fwd_int) ----
  * k_fwin derives each segment's window BEFORE its forward, from the periodized transform of
@@ -195,11 +199,14 @@ struct alignas(256) FslHeader {
      * 785 -> 1361 us with window and counters on shared lines) */
     uint32_t kl, kh, shift;
     uint32_t pad0[29];
-    unsigned long long below[NSHARD]; /* as SelState: below and eq_lo on one line, max on the next */
-    unsigned long long eq_lo[NSHARD];
+    /* per forward workgroup ONE 64-bit add of {keys == kl : keys < kl} (each < 2^32 per tensor)
+     * and one max: per-wave adds of separate counters measured ~9 % of the level-1 forward (the
+     * atomic units' queue on these few lines) */
+    unsigned long long be[NSHARD];
     uint32_t maxkey[NSHARD];
     uint32_t overflow;
-    uint32_t pad1[23];
+    uint32_t pad1[7];
+    uint32_t pad2[32];
 };
 static_assert(sizeof(FslHeader) == 512, "FslHeader lines");
 constexpr int FSL_HDR_WORDS = (int)(sizeof(FslHeader) / 4);
@@ -236,7 +243,12 @@ struct Taps {
 };
 
 /* ---- launchers (kernels.hip) ---- */
-void launch_window(const SegTable& t, SelHeader* head, hipStream_t s);
+void launch_window(const SegTable& t, SelHeader* head, hipStream_t s, const wtp_result* res = nullptr);
+/* the fused selection's retry of the segments whose select read MODE_RETRY (t.retry = 1, chunk
+ * units): k_window, a grid-stride k_collect over their chunks, k_mask_select -- a few us when
+ * no segment missed */
+void launch_fused_retry(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, float* thr_out,
+                        hipStream_t s);
 void launch_collect(const SegTable& t, SelHeader* head, uint32_t* cand, wtp_result* res, hipStream_t s);
 void launch_mask_select(const SegTable& t, SelHeader* head, const uint32_t* cand, wtp_result* res, float* thr_out,
                         hipStream_t s);
