@@ -663,7 +663,12 @@ def main():
                        "parallelism": ("lpt-layer-shard%d+%s" % (world, "allgather-p2p" if args.exchange == "p2p"
                                                                  else "allgather-ring") if sharded
                                        else ("block-split%d" % world if world > 1 else "single")),
-                       "transform": "1-D flattened (extension)" if args.flatten else "2-D over (kh, kw) (reference)"},
+                       "transform": "1-D flattened (extension)" if args.flatten else "2-D over (kh, kw) (reference)",
+                       # wtp_set_fused_select: launch groups of large DWT tensors (cfg5) take their window
+                       # from input patches before the forward and never re-read P for the selection
+                       # (the stage leg's "k_collect" is then k_fslot_collect, its "forward_dwt" includes k_fwin)
+                       "selection": "window / collect / select over P" if args.no_fused_select
+                                    else "fused where a group qualifies (k_fwin, k_fwd_int classification, k_fslot_collect)"},
             "value_source": value_src,
             "timed_region": timed_region,
             "pipeline_hbm_gbs": 8 * n_model / (ms_per_step * 1e-3) / 1e9,

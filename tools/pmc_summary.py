@@ -17,7 +17,8 @@ import re
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_resident", "k_small", "k_mask_select", "k_mask_inplace", "k_collect_t", "k_window", "k_fwd_level", "k_inv_level",
+KERNELS = ["k_resident", "k_small", "k_mask_select", "k_mask_inplace", "k_collect_t", "k_collect_retry", "k_window",
+           "k_fwin", "k_fslot_collect", "k_fwd_level", "k_inv_level",
            "k_fwd_int", "k_inv_int", "k_dwt_cols", "k_dwt_rows",
            "k_idwt_rows", "k_idwt_cols", "k_copy_threshold"]
 

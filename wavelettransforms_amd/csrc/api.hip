@@ -773,13 +773,14 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             any_fused = any_fused || ok;
         }
     }
-    (void)any_fused;
     const int pmode = dwt_groups > 1 ? g_pipeline.load(std::memory_order_relaxed) : 0;
     /* events 2g (group g's forward done) and 2g + 1 (its selection done); the last one joins the
      * side stream back on an error path.  (Round 5's mode 2 -- each group's levels on a lane
      * stream of its own -- measured slower and was removed in round 6; its capture-crash
      * bisection is kept in tools/lanes_capture_diag.py and DESIGN.md.) */
-    const int nev = 2 * ngroups + 1;
+    /* ... and 2 ngroups + g (fused group g's window pass done), 3 ngroups (the call's start, on
+     * the caller's stream) */
+    const int nev = 3 * ngroups + 2;
     SidePipe* pipe = pmode ? side_pipe(s, nev) : nullptr;
     const hipStream_t ss = pipe ? pipe->side : s; /* the selection's stream */
     /* an error after the first fork still joins the side stream back into the caller's (an
@@ -793,10 +794,54 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         }
         return fail(WTP_EHIP, t, "%s", msg);
     };
+    /* the fused groups' window passes (k_fwin) */
+    std::vector<FwinTable> fts(ngroups);
+    for (int gi = 0; gi < ngroups; ++gi) {
+        if (!fused[gi]) continue;
+        FwinTable& ft = fts[gi];
+        memset(&ft, 0, sizeof ft);
+        const int g0 = gi * SEG_PER_LAUNCH, g1 = std::min(ntensors, g0 + SEG_PER_LAUNCH);
+        ft.nseg = g1 - g0;
+        ft.F = tp.F;
+        ft.gh = fwin_hist(head);
+        for (int j = 0; j < tp.F && j < FWIN_F_MAX; ++j) { ft.lo[j] = tp.f[0][j]; ft.hi[j] = tp.f[1][j]; }
+        for (int t = g0; t < g1; ++t) {
+            const TPlan& p = ps[t];
+            FwinSeg& f = ft.s[t - g0];
+            SegDesc sd;
+            memset(&sd, 0, sizeof sd);
+            seg_ranks(p.pop, pct, sd);
+            bucket_plan(p.pop, &sd.nsub_log2, &sd.bucket_cap, true);
+            f.in = tensors[t].in;
+            f.hdr = reinterpret_cast<FslHeader*>(wsb(ws, p.f_off));
+            f.n = p.pop;
+            f.r0 = sd.r0;
+            f.above = sd.above;
+            f.nsub_log2 = sd.nsub_log2;
+            f.B = (int32_t)p.B;
+            f.R = (int32_t)p.g.R[0];
+            f.C = (int32_t)p.g.C[0];
+            f.L = p.L;
+        }
+    }
     if (!pipe) /* group by group: the groups share the level temps (make_layout); a fused group's
                 * forward runs behind its window pass, in the selection loop below */
         for (int gi = 0; gi < ngroups; ++gi)
             if (!fused[gi]) forward_chains(gchains[gi], tp, s);
+    /* pipelined: the first two fused groups' window passes on the side stream ahead of their
+     * forwards (it reads the inputs: it waits for the caller's stream first); group g + 2's
+     * follows group g's selection there, which has read the slot areas g + 2 reuses */
+    auto fwin_side = [&](int gi) {
+        if (gi >= ngroups || !fused[gi]) return true;
+        launch_fwin(fts[gi], head, ss);
+        return hipEventRecord(pipe->ev[2 * ngroups + gi], ss) == hipSuccess;
+    };
+    if (pipe && any_fused) {
+        if (hipEventRecord(pipe->ev[3 * ngroups], s) != hipSuccess || hipStreamWaitEvent(ss, pipe->ev[3 * ngroups], 0) != hipSuccess)
+            return fail_joined(-1, "hipEventRecord / hipStreamWaitEvent failed");
+        forked = true;
+        if (!fwin_side(0) || !fwin_side(1)) return fail_joined(-1, "hipEventRecord failed");
+    }
     /* 2. exact percentile selection + level-0 mask, SEG_PER_LAUNCH segments per launch group:
      * one resident launch when every segment of the group is level-0 and the group's chunks fit
      * the co-resident grid, else window / collect / mask-select */
@@ -871,45 +916,16 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         tab.nblk = blk;
         for (int i = tab.nseg; i < SEG_PER_LAUNCH; ++i) tab.blk_begin[i] = INT32_MAX;
         const bool first = g0 == 0;
-        FwinTable ft;
-        if (fz) {
-            /* fused: the window from the input's patches (into each tensor's slot-area head), the
-             * forward classifying what it writes; then the bucket pass over its slots and the
-             * select, on the side stream when the call is pipelined */
-            memset(&ft, 0, sizeof ft);
-            ft.nseg = tab.nseg;
-            ft.F = tp.F;
-            ft.gh = fwin_hist(head);
-            for (int j = 0; j < tp.F && j < FWIN_F_MAX; ++j) { ft.lo[j] = tp.f[0][j]; ft.hi[j] = tp.f[1][j]; }
-            for (int i = 0; i < tab.nseg; ++i) {
-                const TPlan& p = ps[g0 + i];
-                FwinSeg& f = ft.s[i];
-                f.in = tensors[g0 + i].in;
-                f.hdr = reinterpret_cast<FslHeader*>(wsb(ws, p.f_off));
-                f.n = tab.s[i].n;
-                f.r0 = tab.s[i].r0;
-                f.above = tab.s[i].above;
-                f.nsub_log2 = tab.s[i].nsub_log2;
-                f.B = (int32_t)p.B;
-                f.R = (int32_t)p.g.R[0];
-                f.C = (int32_t)p.g.C[0];
-                f.L = p.L;
-            }
-        }
         if (pipe) { /* this group's forward levels on the caller's stream, its selection behind them */
-            if (fz) {
-                /* group gi - 2 used the same slot areas: its bucket pass has read them */
-                if (gi >= 2 && hipStreamWaitEvent(s, pipe->ev[2 * (gi - 2) + 1], 0) != hipSuccess)
-                    return fail_joined(-1, "hipStreamWaitEvent failed");
-                launch_fwin(ft, head, s);
-            }
+            if (fz && hipStreamWaitEvent(s, pipe->ev[2 * ngroups + gi], 0) != hipSuccess) /* its window */
+                return fail_joined(-1, "hipStreamWaitEvent failed");
             forward_chains(gchains[gi], tp, s, fz);
             if (hipEventRecord(pipe->ev[2 * gi], s) != hipSuccess) return fail_joined(-1, "hipEventRecord failed");
             if (hipStreamWaitEvent(ss, pipe->ev[2 * gi], 0) != hipSuccess)
                 return fail_joined(-1, "hipStreamWaitEvent failed");
             forked = true;
         } else if (fz) {
-            launch_fwin(ft, head, s);
+            launch_fwin(fts[gi], head, s);
             forward_chains(gchains[gi], tp, s, true);
         }
         if (fz) {
@@ -951,6 +967,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         if (pipe && hipEventRecord(pipe->ev[2 * gi + 1], ss) != hipSuccess) {
             return fail_joined(-1, "hipEventRecord failed");
         }
+        if (pipe && !fwin_side(gi + 2)) return fail_joined(-1, "hipEventRecord failed");
     }
     /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2); in
      * the pipelined form group by group, each behind its selection (which joins the side stream) */
