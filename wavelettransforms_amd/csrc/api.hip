@@ -95,10 +95,11 @@ struct TPlan {
 
 struct Layout {
     size_t hist = 0, sel = 0, thr = 0, cand = 0, P = 0, total = 0;
+    size_t fwh = 0; /* k_fwin's histograms (when some tensor can be fused) */
 };
 
 /* persistent slot region: identical position and size in every layout */
-constexpr size_t PERSIST_BYTES = ((sizeof(SelHeader) + 2 * SEL_REGION + FWIN_HIST_BYTES) + 255) / 256 * 256;
+constexpr size_t PERSIST_BYTES = ((sizeof(SelHeader) + 2 * SEL_REGION) + 255) / 256 * 256;
 
 bool pct_ok(double pct) { return pct >= 0.0 && pct <= 100.0; }
 
@@ -312,8 +313,13 @@ Layout make_layout(std::vector<TPlan>& ps, const Taps& tp) {
             fsl_off[k][j] = off;
             off = align_up(off + fsl_words[j] * sizeof(uint32_t));
         }
+    bool anyf = false;
     for (size_t t = 0; t < ps.size(); ++t)
-        if (ps[t].f_slots) ps[t].f_off = fsl_off[(t / SEG_PER_LAUNCH) & 1][t % SEG_PER_LAUNCH];
+        if (ps[t].f_slots) { ps[t].f_off = fsl_off[(t / SEG_PER_LAUNCH) & 1][t % SEG_PER_LAUNCH]; anyf = true; }
+    if (anyf) {
+        L.fwh = off;
+        off = align_up(off + FWIN_HIST_BYTES);
+    }
     L.total = off;
     return L;
 }
@@ -794,7 +800,9 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         }
         return fail(WTP_EHIP, t, "%s", msg);
     };
-    /* the fused groups' window passes (k_fwin) */
+    /* the fused groups' window passes (k_fwin); their histograms start at zero */
+    if (any_fused && hipMemsetAsync(wsb(ws, lay.fwh), 0, FWIN_HIST_BYTES, s) != hipSuccess)
+        return fail(WTP_EHIP, -1, "hipMemsetAsync failed");
     std::vector<FwinTable> fts(ngroups);
     for (int gi = 0; gi < ngroups; ++gi) {
         if (!fused[gi]) continue;
@@ -803,7 +811,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         const int g0 = gi * SEG_PER_LAUNCH, g1 = std::min(ntensors, g0 + SEG_PER_LAUNCH);
         ft.nseg = g1 - g0;
         ft.F = tp.F;
-        ft.gh = fwin_hist(head);
+        ft.gh = reinterpret_cast<uint32_t*>(wsb(ws, lay.fwh));
         for (int j = 0; j < tp.F && j < FWIN_F_MAX; ++j) { ft.lo[j] = tp.f[0][j]; ft.hi[j] = tp.f[1][j]; }
         for (int t = g0; t < g1; ++t) {
             const TPlan& p = ps[t];
@@ -904,9 +912,9 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
                                      (uint64_t)(RES_MS / SAMPLE_GROUP - 1);
             }
             if (late[t - g0]) sd.flags |= SEG_LATE;
-            if (fz) { /* k_fslot_collect: one block per FSC_SLOTS wave slots */
-                sd.fsl = reinterpret_cast<const uint32_t*>(wsb(ws, p.f_off));
-                sd.fsl_n = (int32_t)p.f_slots;
+            if (fz) { /* k_fslot_collect: one block per FSC_SLOTS wave slots (seg_fsl / seg_fsl_n) */
+                sd.out = reinterpret_cast<float*>(wsb(ws, p.f_off));
+                sd.res_step_fx = (uint64_t)p.f_slots;
                 sd.flags |= SEG_FUSED;
                 blk += (int)((p.f_slots + FSC_SLOTS - 1) / FSC_SLOTS);
             } else {
@@ -941,8 +949,8 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
             for (int i = 0; i < rt.nseg; ++i) {
                 SegDesc& sd = rt.s[i];
                 sd.flags &= ~SEG_FUSED;
-                sd.fsl = nullptr;
-                sd.fsl_n = 0;
+                sd.out = nullptr;
+                sd.res_step_fx = 0;
                 sd.blk_begin = rt.blk_begin[i] = rb;
                 rb += (int)((sd.n + CHUNK - 1) / CHUNK);
             }

@@ -889,12 +889,14 @@ __device__ float select_body(const SegDesc& sd, const SelState* __restrict__ st,
         ka = (ca == 1) ? kl : kh;
         kb = (cb == 1) ? kl : kh;
     }
-    if (full && (sd.flags & SEG_FUSED)) {
-        /* a fused segment: its window came from input patches; the retry launches take it again
-         * from P (k_window / k_collect) -- nothing is published here */
-        if (publish && threadIdx.x == 0) res[sd.res].path = MODE_RETRY;
-        __syncthreads();
-        return __uint_as_float(0x7FC00000u);
+    if constexpr (!COH) { /* k_mask_select's select only (k_resident never sees a fused segment) */
+        if (full && (sd.flags & SEG_FUSED)) {
+            /* a fused segment: its window came from input patches; the retry launches take it
+             * again from P (k_window / k_collect) -- nothing is published here */
+            if (publish && threadIdx.x == 0) res[sd.res].path = MODE_RETRY;
+            __syncthreads();
+            return __uint_as_float(0x7FC00000u);
+        }
     }
     if (full) {
         /* the window missed (or a block/bucket overflowed): exact radix select over the segment */
@@ -1265,7 +1267,7 @@ __global__ __launch_bounds__(FSC_THREADS) void k_fslot_collect(SegTable t, SelHe
     const int si = find_seg(t, blockIdx.x);
     const SegDesc& sd = t.s[si];
     SelState* st = sel_region(head, q) + sd.slot;
-    const FslHeader* hd = reinterpret_cast<const FslHeader*>(sd.fsl);
+    const FslHeader* hd = reinterpret_cast<const FslHeader*>(seg_fsl(sd));
     if ((int)blockIdx.x == sd.blk_begin) { /* the segment's first block: the head into the SelState */
         if (threadIdx.x == 0) {
             res[sd.res].zero_count = 0; /* the inverse adds */
@@ -1286,8 +1288,8 @@ __global__ __launch_bounds__(FSC_THREADS) void k_fslot_collect(SegTable t, SelHe
     if (threadIdx.x == 0) s_any = 0;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, hl = lane >> 5, wj = lane & 31;
     const int s0 = ((int)blockIdx.x - sd.blk_begin) * FSC_SLOTS + wv * FSC_SPW;
-    const int ns = max(0, min(FSC_SPW, sd.fsl_n - s0)); /* this wave's slots (uniform) */
-    const uint32_t* base = sd.fsl + FSL_HDR_WORDS + (int64_t)s0 * FSL_WORDS;
+    const int ns = max(0, min(FSC_SPW, seg_fsl_n(sd) - s0)); /* this wave's slots (uniform) */
+    const uint32_t* base = seg_fsl(sd) + FSL_HDR_WORDS + (int64_t)s0 * FSL_WORDS;
     uint32_t w[FSC_NP];
 #pragma unroll
     for (int p = 0; p < FSC_NP; ++p) w[p] = 2 * p + hl < ns ? base[(int64_t)(2 * p + hl) * FSL_WORDS + wj] : 0u;

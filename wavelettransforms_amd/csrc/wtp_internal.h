@@ -93,11 +93,13 @@ struct SegDesc {
     int64_t cap;       /* nsub * bucket_cap                                              */
     int32_t nsub_log2; /* 6..10                                                          */
     int32_t bucket_cap;
-    uint64_t res_step_fx; /* k_resident: (n - SAMPLE_GROUP) / (RES_MS / SAMPLE_GROUP - 1) in 32.32 fixed point */
-    const uint32_t* fsl;  /* fused selection: the segment's slot area (FslHeader, then the wave slots) */
-    int32_t fsl_n;        /* ... and its number of wave slots                              */
-    int32_t pad_f;
+    uint64_t res_step_fx; /* k_resident: (n - SAMPLE_GROUP) / (RES_MS / SAMPLE_GROUP - 1) in 32.32 fixed point;
+                           * SEG_FUSED (k_fslot_collect): the number of wave slots, whose area (FslHeader,
+                           * then the slots) `out` points at -- the SegDesc stays 120 bytes (k_resident's
+                           * kernel argument: a larger table measured +0.2 us there) */
 };
+__host__ __device__ inline const uint32_t* seg_fsl(const SegDesc& sd) { return reinterpret_cast<const uint32_t*>(sd.out); }
+__host__ __device__ inline int32_t seg_fsl_n(const SegDesc& sd) { return (int32_t)sd.res_step_fx; }
 
 struct SegTable {
     int32_t nseg;
@@ -224,16 +226,13 @@ struct FwinSeg {
 struct FwinTable {
     int32_t nseg, F;
     float lo[FWIN_F_MAX], hi[FWIN_F_MAX];
-    uint32_t* gh; /* the persistent histograms (fwin_hist): zero between launches */
+    uint32_t* gh; /* the per-segment histograms (Layout::fwh): zero when the launch starts */
     FwinSeg s[SEG_PER_LAUNCH];
 };
-/* k_fwin's per-segment histogram (NB bins) and arrival counter in the workspace's persistent
- * region (zeroed by wtp_workspace_init; the segment's last patch block re-zeroes what it read) */
+/* k_fwin's per-segment histogram (NB bins) and arrival counter: zeroed once per call that has a
+ * fused group (a memset), re-zeroed by each segment's last patch block for the next group */
 constexpr int FWIN_HW = (NB + 1 + 31) / 32 * 32;
 constexpr size_t FWIN_HIST_BYTES = (size_t)SEG_PER_LAUNCH * FWIN_HW * 4;
-__host__ __device__ inline uint32_t* fwin_hist(void* head) {
-    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(head) + sizeof(SelHeader) + 2 * SEL_REGION);
-}
 
 /* filter taps as a kernel argument (scalar-loaded, uniform across the wave) */
 struct Taps {
