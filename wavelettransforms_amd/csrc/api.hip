@@ -939,6 +939,9 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         if (fz) {
             if (first) { stage(1, ss); stage(2, ss); }
             launch_fslot_collect(tab, head, cand, results, ss);
+            /* group g + 2's window pass next on the side stream: it needs only the slot areas this
+             * bucket pass has read, not this group's select and retry */
+            if (pipe && !fwin_side(gi + 2)) return fail_joined(-1, "hipEventRecord failed");
             if (first) stage(3, ss);
             launch_mask_select(tab, head, cand, results, thr_t, ss);
             /* a segment whose patch window missed the ranks: the unfused window / collect / select
@@ -975,7 +978,7 @@ static int prune_impl(const wtp_tensor* tensors, int ntensors, int wavelet_id, i
         if (pipe && hipEventRecord(pipe->ev[2 * gi + 1], ss) != hipSuccess) {
             return fail_joined(-1, "hipEventRecord failed");
         }
-        if (pipe && !fwin_side(gi + 2)) return fail_joined(-1, "hipEventRecord failed");
+        if (pipe && !fz && !fwin_side(gi + 2)) return fail_joined(-1, "hipEventRecord failed");
     }
     /* 3. inverse transforms with the threshold applied on load (array_to_coeffs + waverec2); in
      * the pipelined form group by group, each behind its selection (which joins the side stream) */
