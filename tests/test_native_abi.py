@@ -149,3 +149,33 @@ def test_integration_stub_is_the_documented_block():
     a = src.index("# --- begin INTEGRATION.md block ---\n") + len("# --- begin INTEGRATION.md block ---\n")
     body = src[a:src.index("# --- end INTEGRATION.md block ---")]
     assert body == block
+
+
+def test_fused_selection_slot_areas_in_the_workspace():
+    """The fused selection's wave slots (k_fwd_int: one 64-word slot per wave of every forward
+    tile, FR x FC = 16 x 56 outputs a tile, 4 waves) plus a 512-byte head per tensor are reserved
+    for a tensor that qualifies (>= 2^22 packed coefficients, tight, images >= 128^2, <= 6 levels,
+    every level with interior tiles) and not for one that does not; a call of more than one launch
+    group holds two sets (group parity) and k_fwin's per-segment histograms."""
+    L = N.lib()
+    wid = L.wtp_wavelet_id(b"db8")
+
+    def ws(shapes, level):
+        return L.wtp_workspace_size_ex(_desc(shapes), len(shapes), wid, level, 0)
+
+    def slots(R, C, level):
+        tot = 0
+        for _ in range(level):
+            Ro, Co = R // 2, C // 2
+            tot += -(-Ro // 16) * -(-Co // 56) * 4
+            R, C = Ro, Co
+        return tot
+
+    head, hist = 512, 24 * 4128 * 4  # FslHeader; SEG_PER_LAUNCH x FWIN_HW words
+    # the same packed size, not fused: level 5's last level (a 128 x 128 input) has no interior tile
+    assert ws([(2048, 2048)], 4) - ws([(2048, 2048)], 5) == 4 * slots(2048, 2048, 4) * 64 + head + hist
+    # non-tight (2048 x 2040 at level 3: 2040 / 8 is not whole) -> nothing reserved
+    assert ws([(2048, 2048)], 3) - ws([(2048, 2040)], 3) >= 4 * slots(2048, 2048, 3) * 64 + head + hist
+    # two groups: two sets of 24 areas
+    big, g1 = ws([(1024, 4096)] * 25, 4), ws([(1024, 4096)] * 24, 4)
+    assert big - g1 >= 24 * (4 * slots(1024, 4096, 4) * 64 + head)
