@@ -700,11 +700,12 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
      * lane of the row pass takes every call (ok = the output exists), so the running count stays
      * the same in all of them. */
     uint32_t f_below = 0, f_eq = 0, f_cnt = 0, f_mx = 0;
+    /* keys <= kl are counted together as "below" (one compare a key): the select then sees no key
+     * at kl, so a rank at or under kl -- ties at the window's lower edge -- reads as a miss and is
+     * retried over P, exactly.  The largest key is kept three at a time (fmax3). */
     auto fcls = [&](float v, bool ok) {
         const uint32_t k = __float_as_uint(v) & 0x7FFFFFFFu;
-        f_below += (uint32_t)__popcll(__ballot(ok && k < skl));
-        f_eq += (uint32_t)__popcll(__ballot(ok && k == skl));
-        f_mx = (ok && k > f_mx) ? k : f_mx;
+        f_below += (uint32_t)__popcll(__ballot(ok && k <= skl));
         const bool in = ok && k - skl - 1u < sspan;
         const uint64_t m = __ballot(in);
         if (m) {
@@ -712,6 +713,11 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
             if (in && pos < (uint32_t)FSL_KEYS) wslot[1 + pos] = k;
             f_cnt += (uint32_t)__popcll(m);
         }
+    };
+    auto fmax3 = [&](float a, float b, float c, bool ok) {
+        const uint32_t m3 = max(max(__float_as_uint(a) & 0x7FFFFFFFu, __float_as_uint(b) & 0x7FFFFFFFu),
+                                __float_as_uint(c) & 0x7FFFFFFFu);
+        f_mx = ok ? max(f_mx, m3) : f_mx;
     };
     if (lane < FC) {
         const __amdgpu_buffer_rsrc_t rP =
@@ -756,7 +762,8 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
                     fcls(hg.x, ok);
                     fcls(lw.y, ok);
                     fcls(hg.y, ok);
-                    if (a.last) fcls(lw.x, ok);
+                    fmax3(hg.x, lw.y, hg.y, ok);
+                    if (a.last) { fcls(lw.x, ok); fmax3(lw.x, lw.x, lw.x, ok); }
                 }
                 if (!ok) continue;
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.x), rA, voff, 4 * r * pitchA, 0);
@@ -801,7 +808,8 @@ __global__ __launch_bounds__(FB_THREADS) WTP_FB_INT_WPE void k_fwd_int(FwdGroup 
                     fcls(hg.x, ok);
                     fcls(lw.y, ok);
                     fcls(hg.y, ok);
-                    if (a.last) fcls(lw.x, ok);
+                    fmax3(hg.x, lw.y, hg.y, ok);
+                    if (a.last) { fcls(lw.x, ok); fmax3(lw.x, lw.x, lw.x, ok); }
                 }
                 if (ok) {
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lw.x), rA, vo, 4 * r * pitchA, 0);
