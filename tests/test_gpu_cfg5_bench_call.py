@@ -1,7 +1,8 @@
 """cfg5 exactly as bench.py runs it (BASELINE configs[4]: 64 x 4096^2 blocks, db8 level 5, the
 50th percentile) in ONE engine.prune call -- three launch groups of 24 / 24 / 16 blocks with the
-selection pipeline on (each group's k_window / k_collect / k_mask_select on the library's side
-stream) -- value-checked on the first and last block of every group against PyWavelets 1.1.1
+selection pipeline on (each group's fused selection -- k_fwin, the forward's classification,
+k_fslot_collect, k_mask_select and the retry launches -- on the library's side stream beside the
+next group's forward) -- value-checked on the first and last block of every group against PyWavelets 1.1.1
 goldens (tools/gen_golden.py --cfg5-groups: output hashes, float64 threshold bits, zero counts),
 out of place and in place.  Reference path: dwt_pruning.py:53-89 per block."""
 import pytest
