@@ -171,3 +171,31 @@ def test_fused_graph_capture_and_replay(eng):
     g.replay()
     torch.cuda.synchronize()
     _same(([o.cpu().numpy() for o in outs], eng.decode(resd, len(xs))), ref)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("fused", [False, True])
+def test_tied_ranks_take_the_batched_full_scan(eng, fused):
+    """Half of a tensor's coefficients exactly +-1.0 (the rest spread): the ranks sit on the tied
+    value, its bucket overflows and k_mask_select takes its exact full-scan radix select (path 3;
+    fused: the retry's, path 11) -- the loop that now keeps 16 loads a thread in flight; level-0
+    tensors (a 1x1 conv weight, resident launch off) count their zeros in the same loop.  Equal
+    to the oracle bit for bit."""
+    prev_res = eng.set_resident(False)
+    try:
+        g = torch.Generator(device="cpu").manual_seed(9)
+        for shape, wavelet, level in (((1024, 4096, 1, 1), "haar", 3), ((2048, 2048), "haar", 1)):
+            xn = torch.randn(shape, generator=g) * 0.3
+            tie = torch.rand(shape, generator=g) < 0.5
+            xn[tie] = torch.where(torch.rand(int(tie.sum()), generator=g) < 0.5, 1.0, -1.0)
+            if len(shape) == 2:  # the tie in the coefficients: haar level 1 of a constant 2x2 block is 2 x
+                xn = xn.repeat_interleave(2, 0)[:shape[0]].repeat_interleave(2, 1)[:, :shape[1]] * 0.5
+            x = xn.cuda()
+            a = _run(eng, [x], fused, wavelet, level, 50.0)
+            ref, rr = O.prune_tensor(xn.numpy(), wavelet, level, 50.0)
+            assert np.array_equal(a[0][0].view(np.uint32), ref.view(np.uint32)), shape
+            assert a[1][0]["zero_count"] == rr["zero_count"]
+            assert G.f64_bits_equal(a[1][0]["thr64"], rr["thr64"])
+            assert a[1][0]["path"] % RETRIED in (MODE_CAND, 2, MODE_FULL), a[1][0]["path"]
+    finally:
+        eng.set_resident(prev_res)
